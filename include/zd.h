@@ -1,0 +1,218 @@
+/*
+ * zd.h — C ABI of the MI355X-native ZSTD block-decode path.
+ *
+ * This is the drop-in boundary for the hot path of the reference crate
+ * AchilleBailly/zstd-decompressor (Rust).  The reference has no FFI of its own;
+ * its boundary is the public Rust API, and each entry point below names the
+ * reference item it replaces (paths relative to the reference repo,
+ * zstd-decompressor/src/…).  A Rust crate binds these with `extern "C"` blocks
+ * (see INTEGRATION.md); the Python mirror in zstd-decompressor_amd/ binds them
+ * with ctypes.
+ *
+ * Conventions
+ *   - Every function returns ZD_OK (0) or a negative ZD_E_* code; nothing
+ *     aborts across the ABI.
+ *   - Plain pointers and sizes only.  `stream` parameters are hipStream_t
+ *     passed as void* (NULL = default stream).
+ *   - "d_" prefixed pointers are device (HBM) pointers, all others host.
+ *   - The caller owns every buffer it passes; objects created by *_create /
+ *     *_new own their own device memory and are released by *_destroy/_free.
+ *   - Objects are not thread-safe; distinct objects may be used from
+ *     distinct threads.
+ */
+#ifndef ZD_H
+#define ZD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZD_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ */
+/* Status codes: one per reference error variant (leaf of the          */
+/* thiserror chain), plus codes for behaviour beyond the reference.    */
+/* ------------------------------------------------------------------ */
+#define ZD_OK 0
+/* parsing::Error (parsing.rs:12-25) */
+#define ZD_E_NOT_ENOUGH_BYTES              (-1)
+#define ZD_E_NOT_ENOUGH_BITS               (-2)
+#define ZD_E_MAX_READABLE_BITS_EXCEEDED    (-3)
+#define ZD_E_EMPTY_INPUT_DATA              (-4)
+#define ZD_E_NULL_BYTE                     (-5)
+#define ZD_E_EMPTY_SLICE                   (-6)
+/* decoders::Error (decoders/mod.rs:10-23) */
+#define ZD_E_LARGE_ACCURACY_LOG            (-12)
+#define ZD_E_CORRUPTED_TABLE               (-13)
+#define ZD_E_SEQUENCE_CODE_MAX_EXCEEDED    (-14)
+/* literals::Error (literals.rs:8-17) */
+#define ZD_E_HUFFMAN_DECODER_MISSING       (-20)
+#define ZD_E_CORRUPTED_STREAMS_SIZE        (-21)
+/* sequences::Error (sequences.rs:14-23) */
+#define ZD_E_SEQ_RESERVED_SET              (-30)
+#define ZD_E_NO_PREVIOUS_DECODER           (-31)
+/* decoding_context::Error (decoding_context.rs:8-15) */
+#define ZD_E_CTX_WINDOW_SIZE_TOO_BIG       (-40)
+#define ZD_E_NULL_OFFSET                   (-41)
+#define ZD_E_IMPOSSIBLE_VALUE              (-42)
+/* block::Error (block.rs:12-25) */
+#define ZD_E_RESERVED_BLOCK_TYPE           (-50)
+/* frame::Error (frame.rs:14-39) */
+#define ZD_E_UNRECOGNIZED_MAGIC            (-60)
+#define ZD_E_FRAME_RESERVED_SET            (-61)
+#define ZD_E_MISSING_CHECKSUM              (-64)
+#define ZD_E_WINDOW_SIZE_TOO_BIG           (-66)
+/* Beyond the reference */
+#define ZD_E_REF_PANIC       (-90) /* the reference would panic / not terminate here */
+#define ZD_E_OUT_OF_DOMAIN   (-91) /* input outside the GPU path's parity domain (DESIGN.md §Parity domain) */
+#define ZD_E_DST_TOO_SMALL   (-92)
+#define ZD_E_INVALID_ARG     (-93)
+#define ZD_E_HIP             (-94) /* a HIP runtime call failed */
+#define ZD_E_NO_MEMORY       (-95)
+#define ZD_E_NOT_DECODED     (-96) /* frame skipped: an earlier frame failed (FrameIterator stops, frame.rs:94-99) */
+
+/* Human-readable name of a status code (static storage). */
+const char* zd_status_name(int status);
+int zd_abi_version(void);
+
+/* ------------------------------------------------------------------ */
+/* Frame index — replaces FrameIterator::next + Frame::parse +        */
+/* Header::parse + Block::parse (frame.rs:61-99,111-177,198-230;       */
+/* block.rs:43-72).  Host-side, O(frames+blocks), reads only headers.  */
+/* ------------------------------------------------------------------ */
+#define ZD_FRAME_ZSTD      0
+#define ZD_FRAME_SKIPPABLE 1
+
+typedef struct zd_frame_desc {
+  uint64_t src_offset;     /* offset of the 4-byte magic in src */
+  uint64_t src_size;       /* bytes of the whole frame (header, blocks, checksum) */
+  uint64_t content_size;   /* Frame_Content_Size, UINT64_MAX if absent */
+  uint64_t window_size;    /* Header::window_size (frame.rs:105) */
+  uint64_t dict_id;        /* Header::dictionnary_id, UINT64_MAX if absent */
+  uint32_t magic;
+  uint32_t kind;           /* ZD_FRAME_ZSTD / ZD_FRAME_SKIPPABLE */
+  uint32_t first_block;    /* index into the block array */
+  uint32_t num_blocks;
+  uint32_t has_checksum;
+  uint32_t checksum;       /* ZStandard::checksum() (frame.rs:268) */
+} zd_frame_desc;
+
+#define ZD_BLOCK_RAW        0
+#define ZD_BLOCK_RLE        1
+#define ZD_BLOCK_COMPRESSED 2
+
+typedef struct zd_block_desc {
+  uint64_t src_offset;     /* first byte after the 3-byte block header */
+  uint32_t block_size;     /* Block_Size field (block.rs:50) */
+  uint8_t  type;           /* ZD_BLOCK_* */
+  uint8_t  last;
+  uint8_t  rle_byte;       /* RLEBlock::byte */
+  uint8_t  _pad;
+} zd_block_desc;
+
+/*
+ * Walk the frames of src[0..n).  Fills up to cap_frames / cap_blocks
+ * descriptors; *nframes / *nblocks receive the totals found (may exceed the
+ * caps: call again with larger arrays).  Stops at the first frame that fails
+ * to parse, like FrameIterator + the CLI loop (src/main.rs:43-53): the
+ * return value is that frame's status and *consumed the byte offset of the
+ * failing frame (n on full success).  Table-level parse errors (FSE/Huffman
+ * descriptions) are found on the GPU, not here.
+ */
+int zd_frames_index(const uint8_t* src, size_t n,
+                    zd_frame_desc* frames, size_t cap_frames, size_t* nframes,
+                    zd_block_desc* blocks, size_t cap_blocks, size_t* nblocks,
+                    size_t* consumed);
+
+/* ------------------------------------------------------------------ */
+/* Batch decode (the hot path): a plan over a byte range of frames.    */
+/* Replaces Frame::decode / ZStandard::decode (frame.rs:79-84,232-260) */
+/* and, per block, Block::decode (block.rs:74-99) with HIP kernels.    */
+/* ------------------------------------------------------------------ */
+typedef struct zd_plan zd_plan;
+
+#define ZD_F_SKIPPABLE  1u  /* append skippable-frame payloads to the output (CLI -p, src/main.rs:45-48) */
+
+typedef struct zd_plan_info {
+  uint64_t nframes;        /* frames in the plan (skippable included) */
+  uint64_t nblocks;
+  uint64_t ncompressed;    /* compressed blocks */
+  uint64_t src_bytes;      /* bytes of src covered by the plan */
+  uint64_t out_bytes;      /* exact decoded size if every frame has a FCS, else an upper bound */
+  uint64_t out_exact;      /* 1 if out_bytes is exact */
+  uint64_t workspace_bytes;/* device workspace owned by the plan */
+  uint64_t nsequences;     /* sum of Number_of_Sequences over compressed blocks */
+  uint64_t nliterals;      /* sum of Regenerated_Size over compressed-literal blocks */
+  int32_t  index_status;   /* status of the host walk (first failing frame) */
+  uint32_t _pad;
+} zd_plan_info;
+
+/* Index src[0..n) on the host and allocate the plan's device workspace.
+ * Host-side work only (no kernel launches).  A frame that fails to index
+ * ends the plan (its status is kept and reported by zd_plan_results). */
+int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out);
+int zd_plan_info_get(const zd_plan* plan, zd_plan_info* info);
+void zd_plan_destroy(zd_plan* plan);
+
+/* Launch the decode pipeline on `stream`.  d_src holds the same n bytes
+ * given to zd_plan_create, resident in HBM; d_dst receives the
+ * concatenated output (>= info.out_bytes).  No host synchronisation, no
+ * allocation: safe to capture in a hipGraph. */
+int zd_decode_async(zd_plan* plan, const uint8_t* d_src, uint8_t* d_dst,
+                    size_t dst_cap, void* stream);
+
+/* After the stream has drained: per-frame status and decoded length
+ * (host arrays of plan nframes entries, either may be NULL), the total
+ * length of the CLI-style output (frames up to the first failure) and the
+ * overall status (first failing frame's status, or ZD_OK).  If some frame
+ * had no FCS this also compacts d_dst in place so the frames are
+ * contiguous (needs the same d_dst and stream). */
+int zd_plan_results(zd_plan* plan, uint8_t* d_dst, void* stream,
+                    int32_t* frame_status, uint64_t* frame_len,
+                    uint64_t* total_len, int32_t* first_error_frame);
+
+/* Per-kernel time of the last zd_decode_async on the plan, in ms (HIP
+ * events recorded between launches when ZD_PROFILE_KERNELS was requested
+ * through zd_plan_set_profiling).  names/ms arrays of cap entries. */
+int zd_plan_set_profiling(zd_plan* plan, int enable);
+int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, int* n);
+
+/* Convenience: host in, host out (H2D + decode + D2H on the default
+ * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
+int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
+                  size_t* out_len, uint32_t flags);
+
+/* ------------------------------------------------------------------ */
+/* DecodingContext mirror (decoding_context.rs:17-106): GPU-resident    */
+/* per-frame state across Block::decode calls.                         */
+/* ------------------------------------------------------------------ */
+typedef struct zd_context zd_context;
+
+/* DecodingContext::new (decoding_context.rs:29-47): fails with
+ * ZD_E_CTX_WINDOW_SIZE_TOO_BIG above 8 MiB. */
+int zd_context_new(uint64_t window_size, zd_context** out);
+void zd_context_free(zd_context* ctx);
+
+/* Block::parse + Block::decode (block.rs:43-99) on the GPU: parses one
+ * block (3-byte header + content) from src[0..n), decodes it on the
+ * device appending to the context.  *consumed / *last as Block::parse. */
+int zd_block_decode(zd_context* ctx, const uint8_t* src, size_t n,
+                    size_t* consumed, int* last);
+
+/* DecodingContext::execute_sequences (decoding_context.rs:78-106) on the
+ * GPU: sequences are (literals_length, offset_value, match_length). */
+int zd_execute_sequences(zd_context* ctx, const uint32_t* ll,
+                         const uint32_t* offset_value, const uint32_t* ml,
+                         size_t nseq, const uint8_t* literals, size_t nlits);
+
+/* DecodingContext::decoded / ::offsets (decoding_context.rs:19-20). */
+int zd_context_decoded(const zd_context* ctx, uint8_t* dst, size_t cap, size_t* len);
+int zd_context_offsets(const zd_context* ctx, uint64_t offsets[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZD_H */
