@@ -1,0 +1,254 @@
+"""Benchmark: decompressed MB/s of the MI355X ZSTD block-decode path.
+
+Workload (default `c4`, BASELINE.json configs[3] at one GPU's share):
+enwik-style synthetic text, 128 KiB independent frames at zstd level 3,
+a 1 GiB unique frame set replicated to 10 GiB decompressed per GPU
+(SURVEY.md §8d allows replication).  One step = one zd_decode_async over the
+whole resident corpus (K1 tables -> K2 Huffman -> K3 FSE -> K4 execute).
+Inputs are resident in HBM before timing; output is verified bit-exact
+against the source bytes after timing.
+
+Multi-GPU: one process per GPU (torchrun), each rank decodes its own
+10 GiB shard — independent frames, no data-path collective (scaling "weak").
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "zstd-decompressor_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_corpus(workload: str, unique_bytes: int, seed: int):
+    from corpus import gen
+    t0 = time.time()
+    if workload == "c2":
+        src = None
+        data = gen.c2_raw_rle(64 << 20)
+        return data, None, 1, {"frames": 1, "frame_bytes": 64 << 20}, time.time() - t0
+    if workload == "c5":
+        src = gen.text(unique_bytes, seed=seed)
+        data = gen.frames(src, 1 << 20, 9)
+        return data, src, None, {"frame_bytes": 1 << 20, "level": 9}, time.time() - t0
+    src = gen.text(unique_bytes, seed=seed)
+    data = gen.frames(src, 128 << 10, 3)
+    return data, src, None, {"frame_bytes": 128 << 10, "level": 3}, time.time() - t0
+
+
+def cpu_baseline(frame_set: bytes, threads: int, budget_s: float = 20.0):
+    """The oracle (C restatement of the reference decoder, kind "port") over a
+    bounded sample of the same frames, frames spread over `threads` threads."""
+    from oracle import oracle
+    from zstd_decompressor.batch import frames_index
+    frames, _, st, _ = frames_index(frame_set)
+    spans = [(f["src_offset"], f["src_size"]) for f in frames]
+    # calibrate on a few frames, then size the sample to ~budget_s of CPU work
+    t0 = time.time()
+    out0 = 0
+    for o, s in spans[:8]:
+        out0 += len(oracle.frame_decode(frame_set[o:o + s])[1])
+    per_byte = (time.time() - t0) / max(out0, 1)
+    want = int(budget_s * threads / max(per_byte, 1e-12))
+    total_out = sum(1 for _ in ())
+    sample, acc = [], 0
+    i = 0
+    while acc < want and i < len(spans) * 4:
+        o, s = spans[i % len(spans)]
+        sample.append((o, s))
+        acc += 128 << 10
+        i += 1
+
+    def work(chunk):
+        n = 0
+        for o, s in chunk:
+            n += len(oracle.frame_decode(frame_set[o:o + s])[1])
+        return n
+
+    parts = [sample[k::threads] for k in range(threads)]
+    t0 = time.time()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        total_out = sum(ex.map(work, parts))
+    dt = time.time() - t0
+    return {"value": round(total_out / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+            "sample": f"{len(sample)} frames ({total_out / 2**20:.0f} MiB decoded) of the same corpus, "
+                      f"oracle/zd_oracle.c on {threads} host threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "c5"])
+    ap.add_argument("--unique-mib", type=int, default=1024, help="unique decompressed MiB per rank before replication")
+    ap.add_argument("--replicas", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import zstd_decompressor as zd
+    from zstd_decompressor.batch import Plan
+
+    # ---- corpus (host), one unique frame set per rank ----
+    frame_set, src, reps_override, meta, tgen = make_corpus(args.workload, args.unique_mib << 20, 0x5EED + 7919 * rank)
+    reps = reps_override or args.replicas
+    data = frame_set * reps
+    log(f"[rank {rank}] corpus: {len(frame_set) / 2**20:.1f} MiB compressed x{reps}, gen {tgen:.1f}s")
+
+    t0 = time.time()
+    plan = Plan(data)
+    info = plan.info
+    log(f"[rank {rank}] plan: {info.nframes} frames, {info.ncompressed} compressed blocks, "
+        f"{info.nsequences} sequences, out {info.out_bytes / 2**30:.2f} GiB, ws {info.workspace_bytes / 2**30:.2f} GiB, "
+        f"{time.time() - t0:.2f}s")
+    assert info.out_exact and info.index_status == 0
+
+    d_src = torch.empty(len(data) + 64, dtype=torch.uint8, device=dev)
+    d_src[: len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    d_dst = torch.empty(info.out_bytes + 64, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step():
+        plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), info.out_bytes, sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    st, total, _, _, first = plan.results(d_dst.data_ptr(), sptr)
+    assert st == 0 and total == info.out_bytes, (st, total, first)
+
+    # ---- timed region ----
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_wall = time.time()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t_wall = time.time() - t_wall
+    if dist:
+        dist.barrier()
+    ms_total = ev0.elapsed_time(ev1)
+    elapsed = torch.tensor([ms_total], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    ms_per_step = float(elapsed.item()) / args.steps
+
+    # ---- per-kernel times (events between launches on the same stream) ----
+    plan.set_profiling(True)
+    kt = {}
+    for _ in range(max(2, min(args.steps, 3))):
+        step()
+        for k, v in plan.kernel_times().items():
+            kt.setdefault(k, []).append(v)
+    plan.set_profiling(False)
+    kt = {k: float(np.mean(v)) for k, v in kt.items()}
+    dom = max(kt, key=kt.get)
+
+    # ---- verify (outside timing) ----
+    verified = None
+    if not args.no_verify and src is not None:
+        st, total, _, _, _ = plan.results(d_dst.data_ptr(), sptr)
+        ref = torch.frombuffer(bytearray(src), dtype=torch.uint8).to(dev)
+        u = len(src)
+        ok = st == 0 and total == u * reps
+        for r in range(reps):
+            ok = ok and bool(torch.equal(d_dst[r * u:(r + 1) * u], ref))
+        verified = bool(ok)
+        del ref
+        assert verified, "GPU output differs from the source bytes"
+
+    out_bytes = info.out_bytes
+    comp_bytes = len(data)
+    total_out = torch.tensor([float(out_bytes)], dtype=torch.float64, device=dev)
+    total_alg = torch.tensor([float(out_bytes + comp_bytes)], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(total_out)
+        dist.all_reduce(total_alg)
+    value = total_out.item() / (ms_per_step / 1e3) / 1e6
+    alg_per_launch = out_bytes + comp_bytes          # C + D, this rank's launch
+    dom_ms = kt[dom]
+    achieved = alg_per_launch / (dom_ms / 1e3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and src is not None:
+        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        cpu = cpu_baseline(frame_set, threads)
+
+    if rank == 0:
+        res = {
+            "metric": "decompressed MB/s (bit-exact vs ref) + % HBM roofline",
+            "value": round(value, 1),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": {"c4": "C4: enwik-style text, 128 KiB frames, zstd -3, 1 GiB unique x10 per GPU",
+                             "c2": "C2: single 64 MiB frame, 512 alternating raw/RLE 128 KiB blocks",
+                             "c5": "C5: text, 1 MiB multi-block frames, zstd -9"}[args.workload],
+                "frames_per_gpu": int(info.nframes),
+                "decompressed_bytes_per_gpu": int(out_bytes),
+                "compressed_bytes_per_gpu": int(comp_bytes),
+                "sequences_per_gpu": int(info.nsequences),
+                "parallelism": f"frame-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "pipeline_achieved": round(alg_per_launch / (ms_per_step / 1e3) / 1e9, 1),
+                "pipeline_frac": round(alg_per_launch / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
+            "cpu_baseline": cpu,
+            "verified_bit_exact": verified,
+        }
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -114,9 +114,11 @@ typedef struct zd_block_desc {
 } zd_block_desc;
 
 /*
- * Walk the frames of src[0..n).  Fills up to cap_frames / cap_blocks
- * descriptors; *nframes / *nblocks receive the totals found (may exceed the
- * caps: call again with larger arrays).  Stops at the first frame that fails
+ * Walk the frames of src[0..n).  With frames == NULL (or cap_frames == 0) the
+ * whole input is walked and *nframes / *nblocks receive the totals (size
+ * query); otherwise at most cap_frames frames are indexed, and blocks beyond
+ * cap_blocks are counted but not stored.  *consumed = bytes of the indexed
+ * frames (Frame::parse advances the parser the same way).  Stops at the first frame that fails
  * to parse, like FrameIterator + the CLI loop (src/main.rs:43-53): the
  * return value is that frame's status and *consumed the byte offset of the
  * failing frame (n on full success).  Table-level parse errors (FSE/Huffman

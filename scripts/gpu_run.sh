@@ -1,0 +1,32 @@
+#!/bin/bash
+# Runs GPU steps on the gpurun box; each step has its own time limit and the
+# script stops at the first fault/abort/timeout (exit 124/134/137/139 or
+# negative signals).  Test failures (pytest exit 1) do not stop later steps.
+# usage: scripts/gpu_run.sh STEP...   (steps: build test smoke bench prof pmc)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139|132|135|136) return 0;; *) return 1;; esac; }
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
+  return $rc
+}
+for s in "$@"; do
+  case "$s" in
+    build) run build 300 python -c "import __graft_entry__ as g; g.build()" || exit 1 ;;
+    test)  run pytest 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testall) run pytest_all 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py ;;
+    benchq) run bench_quick 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,176 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle — the CPU
+restatement of the reference decoder — on the same inputs.
+
+Bit-exact output is required wherever the oracle succeeds; wherever it fails
+the GPU path must fail too, with the same reference error variant (a frame the
+GPU path cannot reproduce reports ZD_E_OUT_OF_DOMAIN, counted separately).
+"""
+import random
+
+import numpy as np
+import pytest
+
+from corpus import gen, libzstd
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+REF_PANIC, OUT_OF_DOMAIN = -90, -91
+
+
+def gpu(data, p=False):
+    from zstd_decompressor.batch import decompress_status
+    return decompress_status(data, p)
+
+
+def assert_parity(data, p=False, what=""):
+    ost, oout = oracle.decompress_status(data, p)
+    gst, gout = gpu(data, p)
+    if ost == 0:
+        assert gst == 0, f"{what}: oracle ok, gpu status {gst}"
+        assert gout == oout, f"{what}: output differs (len {len(gout)} vs {len(oout)})"
+    else:
+        assert gst != 0, f"{what}: oracle status {ost}, gpu ok"
+        if gst != OUT_OF_DOMAIN:
+            assert gst == ost, f"{what}: oracle status {ost}, gpu status {gst}"
+            assert gout == oout, f"{what}: partial output of the frames before the failure differs"
+    return ost, gst
+
+
+def test_kat_frames(kat):
+    for c in kat["frames"]:
+        data = bytes(c["data"])
+        assert_parity(data, False, c["src"])
+        assert_parity(data, True, c["src"])
+
+
+def test_resources(resources):
+    for name, data in resources.items():
+        ost, _ = assert_parity(data, False, name)
+        assert ost == 0
+        assert_parity(data, True, name)
+
+
+def test_execute_sequences_kat(kat):
+    from zstd_decompressor import DecodingContext
+    for c in kat["execute_sequences"]:
+        ctx = DecodingContext(0x42)
+        ctx.execute_sequences([tuple(s) for s in c["seqs"]], bytes(c["literals"]))
+        assert ctx.decoded == bytes(c["out"]), c["src"]
+
+
+def test_context_block_by_block(resources):
+    """Block.parse + Block.decode(ctx) over moby-dick's blocks == Frame.decode
+    (tests/block.rs usage pattern with DecodingContext::new(MAX_WIN_SIZE))."""
+    from zstd_decompressor import ForwardByteParser, Block, DecodingContext, MAX_WIN_SIZE
+    data = resources["moby-dick.txt.zst"]
+    _, expect, _ = oracle.frame_decode(data)
+    p = ForwardByteParser(data)
+    p.slice(4)                                     # magic
+    fhd = p.u8()
+    assert fhd & 0x20 == 0                         # not single segment: window descriptor
+    p.u8()
+    fcs_len = {0: 0, 1: 2, 2: 4, 3: 8}[fhd >> 6]
+    if fcs_len:
+        p.slice(fcs_len)
+    ctx = DecodingContext(MAX_WIN_SIZE)
+    nblocks = 0
+    while True:
+        b, last = Block.parse(p)
+        b.decode(ctx)
+        nblocks += 1
+        if last:
+            break
+    assert nblocks > 1
+    assert ctx.decoded == expect
+
+
+def test_context_window_too_big():
+    from zstd_decompressor import DecodingContext, ZdError
+    with pytest.raises(ZdError) as e:
+        DecodingContext((8 << 20) + 1)
+    assert e.value.name.startswith("WindowSizeTooBig")
+
+
+@pytest.mark.parametrize("kind", ["text", "xml", "binary"])
+@pytest.mark.parametrize("level", [1, 3, 9, 19])
+def test_synthetic_single_block_frames(kind, level):
+    src = {"text": gen.text, "xml": gen.xml, "binary": gen.binary}[kind](1 << 20 if level < 19 else 512 << 10)
+    data = gen.frames(src, 128 << 10, level)
+    ost, gst = assert_parity(data, False, f"{kind} L{level} 128K")
+    assert ost == 0
+    from zstd_decompressor import decompress
+    assert decompress(data) == src
+
+
+@pytest.mark.parametrize("kind", ["text", "xml", "binary"])
+@pytest.mark.parametrize("level", [1, 9, 19])
+def test_synthetic_multi_block_frames(kind, level):
+    """C5 shape: 1 MiB frames of 8 blocks -> Treeless literals, Repeat modes,
+    repeat offsets across blocks, matches into earlier blocks."""
+    n = (2 << 20) if level < 19 else (1 << 20)
+    src = {"text": gen.text, "xml": gen.xml, "binary": gen.binary}[kind](n, seed=level)
+    data = gen.frames(src, 1 << 20, level)
+    ost, gst = assert_parity(data, False, f"{kind} L{level} 1M")
+    assert ost == 0
+
+
+def test_c2_raw_rle():
+    data = gen.c2_raw_rle(8 << 20)
+    ost, gst = assert_parity(data, False, "c2")
+    assert ost == 0
+
+
+def test_checksum_and_no_fcs_frames():
+    src = gen.text(300_000, seed=7)
+    # checksum flag, and a frame without FCS (streaming API absent: emulate by
+    # clearing the FCS flag is not valid; use libzstd output as is + checksum)
+    data = gen.frames(src, 100_000, 3, checksum=True)
+    assert_parity(data, False, "checksum")
+
+
+def test_empty_and_tiny_frames():
+    for n in (1, 2, 3, 5, 17, 100, 1000):
+        src = bytes(random.Random(n).randrange(256) for _ in range(n))
+        assert_parity(libzstd.compress(src, 3), False, f"tiny {n}")
+    assert_parity(libzstd.compress(b"", 3), False, "empty frame (raw block of size 0)")
+    assert_parity(libzstd.compress(b"a" * 100000, 3), False, "rle")
+    assert_parity(libzstd.compress(b"ab" * 100000, 19), False, "period-2")
+
+
+def test_out_of_domain_triggers():
+    """SURVEY §2.1 D2/D3 triggers: the reference fails; so must the GPU path."""
+    r = random.Random(3)
+    letters = bytes(r.choice(b"abcdefghijklmnopqrstuvwxyz") for _ in range(65536))
+    assert_parity(libzstd.compress(letters, 1), False, "D2 random letters L1")
+    two = bytes(r.choice(b"ab") for _ in range(100000))
+    assert_parity(libzstd.compress(two, 3), False, "D3 two symbols")
+    ff = bytes(0xFF if r.random() < 0.5 else r.randrange(256) for _ in range(100000))
+    assert_parity(libzstd.compress(ff, 3), False, "D3 0xFF heavy")
+
+
+def test_corrupted_inputs():
+    """Byte flips / truncations of valid frames: success/failure and error
+    variant parity with the oracle (the reference's fuzz target, fuzz/)."""
+    r = random.Random(1234)
+    src = gen.text(200_000, seed=11)
+    base = gen.frames(src, 64 << 10, 3) + gen.frames(gen.binary(100_000), 50_000, 9)
+    stats = {"ok": 0, "err_same": 0, "ood": 0}
+    for it in range(300):
+        d = bytearray(base)
+        for _ in range(r.randrange(1, 4)):
+            d[r.randrange(len(d))] = r.randrange(256)
+        if r.random() < 0.2:
+            d = d[: r.randrange(len(d))]
+        ost, gst = assert_parity(bytes(d), False, f"corrupt #{it}")
+        stats["ok" if ost == 0 else ("ood" if gst == OUT_OF_DOMAIN else "err_same")] += 1
+    assert stats["ok"] + stats["err_same"] >= 290, stats
+
+
+def test_many_frame_roundtrip_large():
+    """Size-independent property at a larger size: decode(compress(x)) == x,
+    and the per-frame statuses are all OK."""
+    src = gen.text(64 << 20, seed=99)
+    data = gen.frames(src, 128 << 10, 3)
+    from zstd_decompressor import decompress
+    assert decompress(data) == src

@@ -1,0 +1,1059 @@
+// zd_host.cpp — host planner and C ABI (include/zd.h).
+//
+// The host does what the reference's parse phase does with headers only
+// (FrameIterator / Frame::parse / Header::parse / Block::parse and the
+// fixed-size parts of LiteralsSection::parse and Sequences::parse), resolves
+// which block's Huffman/FSE tables every block uses (Treeless literals,
+// Repeat_Mode) and carves the device workspace.  Everything that reads
+// entropy-coded data — Huffman/FSE table descriptions, literal streams,
+// sequence bitstreams, the LZ77 execute — runs in the HIP kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/zd.h"
+#include "zd_common.h"
+#include "zd_launch.h"
+
+using namespace zd;
+
+namespace {
+
+constexpr uint32_t MAGIC_ZSTD = 0xFD2FB528u;   // frame.rs:41
+constexpr uint32_t MAGIC_SKIP = 0x184D2A50u;   // frame.rs:42
+
+struct Err {
+  int code = 0;
+  uint32_t stage = PS_STRUCT;
+};
+
+// ForwardByteParser (parsing.rs:9-112)
+struct Bytes {
+  const uint8_t* p;
+  size_t n;
+  int u8(uint8_t* v) {
+    if (!n) return ZD_E_NOT_ENOUGH_BYTES;
+    *v = *p++; n--; return 0;
+  }
+  int slice(size_t len, const uint8_t** s) {
+    if (len == 0) return ZD_E_EMPTY_SLICE;
+    if (n < len) return ZD_E_NOT_ENOUGH_BYTES;
+    *s = p; p += len; n -= len; return 0;
+  }
+  int le(size_t k, uint64_t* v) {
+    if (n < k) return ZD_E_NOT_ENOUGH_BYTES;
+    uint64_t r = 0;
+    for (size_t i = 0; i < k; i++) r |= (uint64_t)p[i] << (8 * i);
+    p += k; n -= k; *v = r; return 0;
+  }
+};
+
+struct HostBlock {
+  uint64_t src;          // absolute offset of the block content
+  uint32_t size;
+  uint8_t type, last, rle;
+  // compressed only
+  CompBlock cb;
+};
+
+struct HostFrame {
+  zd_frame_desc d;
+  std::vector<HostBlock> blocks;
+  uint64_t key = KEY_NONE;    // host-detected parse error (frame stops here)
+  int status = 0;
+};
+
+// Literals section header + the host-visible parts of the section
+// (literals.rs:88-206) and of the sequences header (sequences.rs:52-87 and
+// the mode byte of 91-143).  `c` spans the block content.
+int parse_compressed(const uint8_t* base, uint64_t off, uint32_t size, CompBlock* cb, Err* e) {
+  Bytes np{base + off, size};
+  const uint8_t* start = np.p;
+  auto rel = [&]() { return (uint32_t)(np.p - start); };
+  e->stage = PS_STRUCT;
+  uint8_t h;
+  if (int r = np.u8(&h)) return e->code = r;
+  int lt = h & 3, sf = (h >> 2) & 3;
+  uint32_t regen = 0, csize = 0;
+  int nstreams = 1;
+  if (lt == LIT_RAW || lt == LIT_RLE) {
+    uint8_t b1, b2;
+    if (sf == 0 || sf == 2) regen = h >> 3;
+    else if (sf == 1) { if (int r = np.u8(&b1)) return e->code = r; regen = (h >> 4) + ((uint32_t)b1 << 4); }
+    else {
+      if (int r = np.u8(&b1)) return e->code = r;
+      if (int r = np.u8(&b2)) return e->code = r;
+      regen = (h >> 4) + ((uint32_t)b1 << 4) + ((uint32_t)b2 << 12);
+    }
+  } else {
+    const uint8_t* s;
+    uint32_t nb = sf <= 1 ? 2 : (uint32_t)sf + 1;
+    if (int r = np.slice(nb, &s)) return e->code = r;
+    uint32_t x = 0;
+    for (uint32_t i = 0; i < nb; i++) x |= (uint32_t)s[i] << (8 * i);
+    if (sf <= 1) { regen = (h >> 4) + ((x & 0x3F) << 4); csize = x >> 6; nstreams = sf == 0 ? 1 : 4; }
+    else if (sf == 2) { regen = (h >> 4) + ((x & 0x3FF) << 4); csize = (x >> 10) & 0x3FFF; nstreams = 4; }
+    else { regen = (h >> 4) + ((x & 0x3FFF) << 4); csize = (x >> 14) & 0x3FFFF; nstreams = 4; }
+  }
+  cb->lit_type = (uint8_t)lt;
+  cb->lit_regen = regen;
+  cb->nstreams = 0;
+  if (lt == LIT_RAW) {
+    const uint8_t* s;
+    cb->lit_data = rel();
+    if (int r = np.slice(regen, &s)) return e->code = r;
+  } else if (lt == LIT_RLE) {
+    if (int r = np.u8(&cb->lit_rle)) return e->code = r;
+  } else {
+    const uint8_t* cs;
+    if (int r = np.slice(csize, &cs)) return e->code = r;
+    Bytes ni{cs, csize};
+    const uint8_t* ni_start = cs;
+    if (lt == LIT_COMPRESSED) {      // HuffmanDecoder::parse header + description slice (huffman.rs:80-130)
+      e->stage = PS_HUF_DESC;
+      cb->lit_data = (uint32_t)(cs - start);
+      uint8_t hh;
+      if (int r = ni.u8(&hh)) return e->code = r;
+      size_t dl = hh < 128 ? hh : ((size_t)(hh - 127) / 2 + (hh - 127) % 2);
+      const uint8_t* d;
+      if (int r = ni.slice(dl, &d)) return e->code = r;
+      cb->huf_desc_size = (uint32_t)(1 + dl);
+    }
+    e->stage = PS_JUMP;
+    size_t total = ni.n;
+    uint32_t ss[4] = {0, 0, 0, 0};
+    if (nstreams == 4) {
+      uint64_t s1, s2, s3;
+      if (int r = ni.le(2, &s1)) return e->code = r;
+      if (int r = ni.le(2, &s2)) return e->code = r;
+      if (int r = ni.le(2, &s3)) return e->code = r;
+      if (s1 + s2 + s3 > total - 6) return e->code = ZD_E_CORRUPTED_STREAMS_SIZE;
+      size_t s4 = total - 6 - s1 - s2 - s3;
+      ss[0] = (uint32_t)s1; ss[1] = (uint32_t)s2; ss[2] = (uint32_t)s3; ss[3] = (uint16_t)s4;
+    } else {
+      ss[0] = (uint16_t)ni.n;
+    }
+    cb->streams = (uint32_t)(ni.p - start);
+    const uint8_t* d;
+    if (int r = ni.slice(ni.n, &d)) return e->code = r;
+    (void)ni_start;
+    // literals.rs:70-73: the stream loop stops at the first empty stream
+    for (int k = 0; k < 4; k++) {
+      if (ss[k] == 0) break;
+      cb->stream_size[k] = ss[k];
+      cb->nstreams = (uint8_t)(k + 1);
+    }
+  }
+  // Sequences::parse (sequences.rs:52-75)
+  e->stage = PS_SEQ_HDR;
+  uint8_t b0;
+  if (int r = np.u8(&b0)) return e->code = r;
+  uint32_t nseq;
+  if (b0 == 0) nseq = 0;
+  else if (b0 < 128) nseq = b0;
+  else if (b0 < 255) { uint8_t b1; if (int r = np.u8(&b1)) return e->code = r; nseq = ((uint32_t)(b0 - 128) << 8) + b1; }
+  else {
+    uint8_t b1, b2;
+    if (int r = np.u8(&b1)) return e->code = r;
+    if (int r = np.u8(&b2)) return e->code = r;
+    nseq = (uint32_t)b1 + ((uint32_t)b2 << 8) + 0x7F;     // D1 (sequences.rs:84)
+  }
+  cb->nseq = nseq;
+  cb->modes[0] = cb->modes[1] = cb->modes[2] = M_REPEAT;
+  if (nseq) {
+    const uint8_t* mb;
+    if (int r = np.slice(1, &mb)) return e->code = r;
+    if (mb[0] & 3) return e->code = ZD_E_SEQ_RESERVED_SET;
+    cb->modes[0] = (mb[0] >> 6) & 3;
+    cb->modes[1] = (mb[0] >> 4) & 3;
+    cb->modes[2] = (mb[0] >> 2) & 3;
+  }
+  cb->seq_tables = rel();
+  return 0;
+}
+
+// Header::parse (frame.rs:111-177)
+int parse_header(Bytes& in, zd_frame_desc* f) {
+  const uint8_t* b;
+  if (int r = in.slice(1, &b)) return r;
+  unsigned fhd = b[0];
+  unsigned dict_flag = fhd & 3, csum = (fhd >> 2) & 1, reserved = (fhd >> 3) & 1;
+  unsigned single = (fhd >> 5) & 1, fcs_flag = fhd >> 6;
+  if (reserved) return ZD_E_FRAME_RESERVED_SET;
+  int fcs_size = (fcs_flag == 0) ? (single ? 1 : -1) : (1 << fcs_flag);
+  uint64_t window = 0;
+  if (!single) {
+    uint8_t wd;
+    if (int r = in.u8(&wd)) return r;
+    uint64_t base = 1ull << ((wd >> 3) + 10);
+    window = base + (base / 8) * (wd & 7);
+  }
+  f->dict_id = UINT64_MAX;
+  if (dict_flag) {
+    const uint8_t* a;
+    size_t dl = (size_t)1 << (dict_flag - 1);
+    if (int r = in.slice(dl, &a)) return r;
+    uint64_t v = 0;
+    for (size_t i = 0; i < dl; i++) v |= (uint64_t)a[i] << (8 * i);
+    f->dict_id = v;
+  }
+  f->content_size = UINT64_MAX;
+  if (fcs_size > 0) {
+    const uint8_t* a;
+    if (int r = in.slice((size_t)fcs_size, &a)) return r;
+    uint64_t v = 0;
+    for (int i = 0; i < fcs_size; i++) v |= (uint64_t)a[i] << (8 * i);
+    if (fcs_size == 2) v += 256;
+    f->content_size = v;
+  }
+  f->window_size = single ? f->content_size : window;
+  f->has_checksum = csum;
+  return 0;
+}
+
+// Walks one frame at in.  On error, hf->key/status hold the failure; blocks
+// parsed before (and the failing one, with its host_stage) are kept.
+int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf) {
+  zd_frame_desc& f = hf->d;
+  memset(&f, 0, sizeof f);
+  f.src_offset = (uint64_t)(in.p - base);
+  f.content_size = UINT64_MAX;
+  f.dict_id = UINT64_MAX;
+  auto fail = [&](int code, uint32_t blk, uint32_t stage) {
+    hf->status = code;
+    hf->key = make_key(PH_PARSE, blk, stage, 0, code);
+    f.src_size = (uint64_t)(in.p - base) - f.src_offset;
+    return code;
+  };
+  uint64_t magic;
+  if (int r = in.le(4, &magic)) return fail(r, 0, PS_STRUCT);
+  f.magic = (uint32_t)magic;
+  if (f.magic == MAGIC_ZSTD) {
+    f.kind = ZD_FRAME_ZSTD;
+    if (int r = parse_header(in, &f)) return fail(r, 0, PS_STRUCT);
+    if (f.window_size > MAX_WIN_SIZE) return fail(ZD_E_WINDOW_SIZE_TOO_BIG, 0, PS_STRUCT);
+    for (uint32_t bi = 0;; bi++) {
+      const uint8_t* h;
+      if (int r = in.slice(3, &h)) return fail(r, bi, PS_STRUCT);
+      uint32_t x = h[0] | (h[1] << 8) | ((uint32_t)h[2] << 16);
+      HostBlock hb;
+      memset(&hb, 0, sizeof hb);
+      hb.last = x & 1;
+      hb.type = (x >> 1) & 3;
+      hb.size = x >> 3;
+      hb.src = (uint64_t)(in.p - base);
+      if (hb.type == 0) {
+        const uint8_t* s;
+        if (int r = in.slice(hb.size, &s)) return fail(r, bi, PS_STRUCT);
+      } else if (hb.type == 1) {
+        if (int r = in.u8(&hb.rle)) return fail(r, bi, PS_STRUCT);
+      } else if (hb.type == 2) {
+        const uint8_t* s;
+        if (int r = in.slice(hb.size, &s)) return fail(r, bi, PS_STRUCT);
+        CompBlock& cb = hb.cb;
+        cb.src = hb.src;
+        cb.size = hb.size;
+        cb.block_in_frame = bi;
+        cb.host_stage = PS_ALL;
+        Err e;
+        int r = parse_compressed(base, hb.src, hb.size, &cb, &e);
+        if (r) {
+          cb.host_stage = (uint8_t)e.stage;
+          hf->blocks.push_back(hb);
+          return fail(r, bi, e.stage);
+        }
+      } else {
+        return fail(ZD_E_RESERVED_BLOCK_TYPE, bi, PS_STRUCT);
+      }
+      hf->blocks.push_back(hb);
+      if (hb.last) break;
+    }
+    if (f.has_checksum) {
+      uint64_t cs;
+      if (in.le(4, &cs)) return fail(ZD_E_MISSING_CHECKSUM, (uint32_t)hf->blocks.size(), PS_STRUCT);
+      f.checksum = (uint32_t)cs;
+    }
+  } else if ((f.magic ^ MAGIC_SKIP) <= 0x0F) {
+    f.kind = ZD_FRAME_SKIPPABLE;
+    uint64_t len;
+    if (int r = in.le(4, &len)) return fail(r, 0, PS_STRUCT);
+    const uint8_t* s;
+    HostBlock hb;
+    memset(&hb, 0, sizeof hb);
+    hb.src = (uint64_t)(in.p - base);
+    if (int r = in.slice((size_t)len, &s)) return fail(r, 0, PS_STRUCT);
+    hb.type = 4;
+    hb.size = (uint32_t)len;
+    hb.last = 1;
+    hf->blocks.push_back(hb);
+  } else {
+    return fail(ZD_E_UNRECOGNIZED_MAGIC, 0, PS_STRUCT);
+  }
+  f.src_size = (uint64_t)(in.p - base) - f.src_offset;
+  return 0;
+}
+
+#define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { \
+  fprintf(stderr, "zd: %s failed: %s\n", #x, hipGetErrorString(_e)); return ZD_E_HIP; } } while (0)
+
+}  // namespace
+
+// ===========================================================================
+// Plan
+// ===========================================================================
+struct zd_plan {
+  uint32_t flags = 0;
+  std::vector<HostFrame> frames;
+  std::vector<CompBlock> comps;
+  std::vector<BlockRec> blocks;
+  std::vector<FrameDesc> fdesc;
+  std::vector<FrameState> fstate0;
+  std::vector<uint32_t> list_tables, list_huf, list_seq;
+  std::vector<uint64_t> frame_cap_off;   // output offset per frame (capacity layout)
+  zd_plan_info info{};
+  Workspace W{};
+  uint8_t* d_ws = nullptr;
+  uint8_t* d_staging = nullptr;          // when the output layout is not exact
+  uint64_t staging_bytes = 0;
+  int index_status = 0;
+  size_t index_stop = 0;                 // frame index that failed to index (== frames.size()-1) or frames.size()
+  bool profile = false;
+  hipEvent_t ev[N_KERNELS + 1] = {};
+  bool ev_made = false;
+  bool launched = false;
+  // context API hook: comp 0 is a prebuilt "previous block" carrying tables
+  bool has_prebuilt = false;
+};
+
+namespace {
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// Builds device-side descriptors from the host frames.  `prev_*` seed the
+// Treeless/Repeat resolution (context API), -1 when absent.
+int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
+               const uint64_t rep0[3], uint64_t fixed_cap) {
+  uint64_t lits = 0, nseq_total = 0, out_off = 0;
+  uint32_t lut_slots = 0, fse_slots = 0;
+  bool exact = true;
+  P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear();
+  P->frame_cap_off.clear();
+  for (size_t fi = 0; fi < P->frames.size(); fi++) {
+    HostFrame& hf = P->frames[fi];
+    FrameDesc fd{};
+    FrameState fs{};
+    fs.key = hf.key;
+    fs.rep[0] = rep0[0]; fs.rep[1] = rep0[1]; fs.rep[2] = rep0[2];
+    fd.first_block = (uint32_t)P->blocks.size();
+    fd.out_len0 = out_len0;
+    int32_t huf_prev = prev_huf;
+    int32_t tab_prev[3] = {prev_tab[0], prev_tab[1], prev_tab[2]};
+    uint64_t bound = 0;
+    bool frame_failed_host = hf.key != KEY_NONE;
+    for (size_t bi = 0; bi < hf.blocks.size(); bi++) {
+      HostBlock& hb = hf.blocks[bi];
+      BlockRec br{};
+      br.src = hb.src; br.size = hb.size; br.type = hb.type; br.last = hb.last; br.rle = hb.rle; br.comp = -1;
+      if (hb.type == 2) {
+        CompBlock cb = hb.cb;
+        cb.frame = (uint32_t)fi;
+        cb.block_in_frame = (uint32_t)bi;
+        cb.prebuilt = 0;
+        cb.huf_src = -1;
+        cb.tab_src[0] = cb.tab_src[1] = cb.tab_src[2] = -1;
+        uint32_t ci = (uint32_t)P->comps.size();
+        bool failing = cb.host_stage != PS_ALL;
+        // literals: Treeless resolution (literals.rs:59-66)
+        if (!failing && (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS)) {
+          if (cb.lit_type == LIT_COMPRESSED) { cb.huf_src = (int32_t)ci; huf_prev = (int32_t)ci; }
+          else cb.huf_src = huf_prev;
+          if (cb.huf_src < 0)
+            fs.key = std::min(fs.key, make_key(PH_DECODE, (uint32_t)bi, DS_LITERALS, 0, ZD_E_HUFFMAN_DECODER_MISSING));
+        }
+        if (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) cb.lut_slot = lut_slots++;
+        // sequences: Repeat resolution (sequences.rs:147-187, 232-234)
+        if (!failing) {
+          if (cb.nseq == 0) {
+            int code = ZD_E_EMPTY_INPUT_DATA;
+            for (int k = 0; k < 3; k++) if (tab_prev[k] < 0) { code = ZD_E_NO_PREVIOUS_DECODER; break; }
+            fs.key = std::min(fs.key, make_key(PH_DECODE, (uint32_t)bi, DS_SEQUENCES, 0, code));
+          } else {
+            cb.fse_slot = fse_slots++;
+            bool miss = false;
+            for (int k = 0; k < 3; k++) {
+              if (cb.modes[k] == M_REPEAT) {
+                if (tab_prev[k] < 0) { miss = true; break; }
+                cb.tab_src[k] = tab_prev[k];
+              } else {
+                cb.tab_src[k] = (int32_t)ci;
+              }
+            }
+            if (miss) fs.key = std::min(fs.key, make_key(PH_DECODE, (uint32_t)bi, DS_SEQUENCES, 0, ZD_E_NO_PREVIOUS_DECODER));
+            else for (int k = 0; k < 3; k++) tab_prev[k] = cb.tab_src[k];
+          }
+        } else if (cb.nseq) {
+          cb.fse_slot = fse_slots++;
+        }
+        // workspace
+        if (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) {
+          cb.lit_out = lits;
+          lits += align_up((uint64_t)cb.lit_regen + 16, 16);
+        }
+        cb.seq_out = nseq_total;
+        nseq_total += cb.nseq;
+        P->comps.push_back(cb);
+        br.comp = (int32_t)ci;
+        bool needs_tables = (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) ||
+                            (cb.nseq > 0 && cb.host_stage > PS_SEQ_TABLES);
+        if (needs_tables) P->list_tables.push_back(ci);
+        if (!frame_failed_host) {
+          if ((cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) && cb.nstreams && cb.huf_src >= 0)
+            P->list_huf.push_back(ci);
+          if (cb.nseq > 0 && cb.tab_src[0] >= 0 && cb.tab_src[1] >= 0 && cb.tab_src[2] >= 0)
+            P->list_seq.push_back(ci);
+        }
+        bound += MAX_BLOCK_OUT;
+      } else {
+        bound += hb.size;
+      }
+      P->blocks.push_back(br);
+    }
+    fd.nblocks = (uint32_t)hf.blocks.size();
+    uint64_t cap;
+    if (hf.d.kind == ZD_FRAME_SKIPPABLE) {
+      cap = (P->flags & ZD_F_SKIPPABLE) ? hf.blocks[0].size : 0;
+      if (!(P->flags & ZD_F_SKIPPABLE)) fd.nblocks = 0;
+    } else if (hf.d.content_size != UINT64_MAX && hf.d.content_size <= bound) {
+      cap = hf.d.content_size;
+    } else {
+      cap = bound;
+      exact = false;
+    }
+    if (frame_failed_host) fd.nblocks = 0;
+    if (fixed_cap) cap = fixed_cap;
+    fd.out = out_off;
+    fd.out_cap = cap;
+    P->frame_cap_off.push_back(out_off);
+    out_off += cap;
+    P->fdesc.push_back(fd);
+    P->fstate0.push_back(fs);
+  }
+  // workspace carve-up
+  Workspace& W = P->W;
+  uint64_t o = 0;
+  auto carve = [&](uint64_t bytes) { uint64_t r = o; o = align_up(o + bytes, 256); return r; };
+  W.comp = carve(sizeof(CompBlock) * std::max<size_t>(P->comps.size(), 1));
+  W.comp_state = carve(sizeof(CompState) * std::max<size_t>(P->comps.size(), 1));
+  W.blocks = carve(sizeof(BlockRec) * std::max<size_t>(P->blocks.size(), 1));
+  W.frames = carve(sizeof(FrameDesc) * std::max<size_t>(P->fdesc.size(), 1));
+  W.frame_state = carve(sizeof(FrameState) * std::max<size_t>(P->fdesc.size(), 1));
+  W.list_tables = carve(4 * std::max<size_t>(P->list_tables.size(), 1));
+  W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
+  W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
+  W.lits = carve(lits + 64);
+  W.seq_ll = carve(4 * nseq_total + 64);
+  W.seq_of = carve(4 * nseq_total + 64);
+  W.seq_ml = carve(4 * nseq_total + 64);
+  W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
+  W.fses = carve((uint64_t)FSE_ENTRIES * 4 * 3 * std::max<uint32_t>(fse_slots, 1));
+  W.total = o;
+
+  zd_plan_info& I = P->info;
+  I.nframes = P->fdesc.size();
+  I.nblocks = P->blocks.size();
+  I.ncompressed = P->comps.size();
+  I.out_bytes = out_off;
+  I.out_exact = exact;
+  I.workspace_bytes = W.total;
+  I.nsequences = nseq_total;
+  I.nliterals = lits;
+  I.index_status = P->index_status;
+  return 0;
+}
+
+int upload_plan(zd_plan* P) {
+  HIPCHK(hipMalloc(&P->d_ws, P->W.total));
+  auto up = [&](uint64_t off, const void* p, size_t bytes) -> int {
+    if (bytes) HIPCHK(hipMemcpy(P->d_ws + off, p, bytes, hipMemcpyHostToDevice));
+    return 0;
+  };
+  if (int r = up(P->W.comp, P->comps.data(), P->comps.size() * sizeof(CompBlock))) return r;
+  if (int r = up(P->W.blocks, P->blocks.data(), P->blocks.size() * sizeof(BlockRec))) return r;
+  if (int r = up(P->W.frames, P->fdesc.data(), P->fdesc.size() * sizeof(FrameDesc))) return r;
+  if (int r = up(P->W.list_tables, P->list_tables.data(), P->list_tables.size() * 4)) return r;
+  if (int r = up(P->W.list_huf, P->list_huf.data(), P->list_huf.size() * 4)) return r;
+  if (int r = up(P->W.list_seq, P->list_seq.data(), P->list_seq.size() * 4)) return r;
+  if (!P->info.out_exact) {
+    P->staging_bytes = P->info.out_bytes;
+    HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
+  }
+  return 0;
+}
+
+int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
+  Bytes in{src, n};
+  while (in.n) {                              // FrameIterator::next (frame.rs:94-99)
+    HostFrame hf;
+    int r = index_frame(src, in, &hf);
+    P->frames.push_back(std::move(hf));
+    if (r) { P->index_status = r; break; }
+  }
+  P->index_stop = P->frames.size();
+  return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int zd_abi_version(void) { return ZD_ABI_VERSION; }
+
+const char* zd_status_name(int s) {
+  switch (s) {
+    case ZD_OK: return "Ok";
+    case ZD_E_NOT_ENOUGH_BYTES: return "NotEnoughBytes";
+    case ZD_E_NOT_ENOUGH_BITS: return "NotEnoughBits";
+    case ZD_E_MAX_READABLE_BITS_EXCEEDED: return "MaximumReadableBitsExceeded";
+    case ZD_E_EMPTY_INPUT_DATA: return "EmptyInputData";
+    case ZD_E_NULL_BYTE: return "NullByte";
+    case ZD_E_EMPTY_SLICE: return "EmptySliceError";
+    case ZD_E_LARGE_ACCURACY_LOG: return "LargeAccuracyLog";
+    case ZD_E_CORRUPTED_TABLE: return "CorruptedTable";
+    case ZD_E_SEQUENCE_CODE_MAX_EXCEEDED: return "SequenceCodeMaxValueExceeded";
+    case ZD_E_HUFFMAN_DECODER_MISSING: return "HuffmanDecoderMissing";
+    case ZD_E_CORRUPTED_STREAMS_SIZE: return "CorruptedStreamsSizeTooBig";
+    case ZD_E_SEQ_RESERVED_SET: return "ReservedSet(sequences)";
+    case ZD_E_NO_PREVIOUS_DECODER: return "NoPreviousDecoder";
+    case ZD_E_CTX_WINDOW_SIZE_TOO_BIG: return "WindowSizeTooBig(context)";
+    case ZD_E_NULL_OFFSET: return "NullOffsetError";
+    case ZD_E_IMPOSSIBLE_VALUE: return "ImpossibleValue";
+    case ZD_E_RESERVED_BLOCK_TYPE: return "ReservedBlockType";
+    case ZD_E_UNRECOGNIZED_MAGIC: return "UnrecognizedMagic";
+    case ZD_E_FRAME_RESERVED_SET: return "ReservedSet(frame)";
+    case ZD_E_MISSING_CHECKSUM: return "MissingChecksum";
+    case ZD_E_WINDOW_SIZE_TOO_BIG: return "WindowSizeTooBig";
+    case ZD_E_REF_PANIC: return "ReferencePanic";
+    case ZD_E_OUT_OF_DOMAIN: return "OutOfDomain";
+    case ZD_E_DST_TOO_SMALL: return "DstTooSmall";
+    case ZD_E_INVALID_ARG: return "InvalidArgument";
+    case ZD_E_HIP: return "HipError";
+    case ZD_E_NO_MEMORY: return "NoMemory";
+    case ZD_E_NOT_DECODED: return "NotDecoded";
+    default: return "Unknown";
+  }
+}
+
+int zd_frames_index(const uint8_t* src, size_t n, zd_frame_desc* frames, size_t cap_frames, size_t* nframes,
+                    zd_block_desc* blocks, size_t cap_blocks, size_t* nblocks, size_t* consumed) {
+  if (!src && n) return ZD_E_INVALID_ARG;
+  Bytes in{src, n};
+  size_t nf = 0, nb = 0;
+  int status = 0;
+  size_t stop = n;
+  while (in.n) {
+    if (frames && cap_frames && nf >= cap_frames) { stop = (size_t)(in.p - src); break; }
+    HostFrame hf;
+    size_t at = (size_t)(in.p - src);
+    int r = index_frame(src, in, &hf);
+    if (r) { status = r; stop = at; break; }
+    hf.d.first_block = (uint32_t)nb;
+    hf.d.num_blocks = (uint32_t)hf.blocks.size();
+    if (frames && nf < cap_frames) frames[nf] = hf.d;
+    for (auto& b : hf.blocks) {
+      if (blocks && nb < cap_blocks) {
+        zd_block_desc& d = blocks[nb];
+        d.src_offset = b.src; d.block_size = b.size; d.type = b.type == 4 ? 0 : b.type;
+        d.last = b.last; d.rle_byte = b.rle; d._pad = 0;
+      }
+      nb++;
+    }
+    nf++;
+  }
+  if (nframes) *nframes = nf;
+  if (nblocks) *nblocks = nb;
+  if (consumed) *consumed = stop;
+  return status;
+}
+
+int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) {
+  if (!out || (!src && n)) return ZD_E_INVALID_ARG;
+  zd_plan* P = new (std::nothrow) zd_plan();
+  if (!P) return ZD_E_NO_MEMORY;
+  P->flags = flags;
+  plan_index(P, src, n);
+  int32_t none[3] = {-1, -1, -1};
+  uint64_t rep0[3] = {1, 4, 8};
+  build_plan(P, -1, none, 0, rep0, 0);
+  P->info.src_bytes = n;
+  int r = upload_plan(P);
+  if (r) { zd_plan_destroy(P); return r; }
+  *out = P;
+  return ZD_OK;
+}
+
+int zd_plan_info_get(const zd_plan* P, zd_plan_info* info) {
+  if (!P || !info) return ZD_E_INVALID_ARG;
+  *info = P->info;
+  return ZD_OK;
+}
+
+void zd_plan_destroy(zd_plan* P) {
+  if (!P) return;
+  if (P->d_ws) (void)hipFree(P->d_ws);
+  if (P->d_staging) (void)hipFree(P->d_staging);
+  if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
+  delete P;
+}
+
+int zd_plan_set_profiling(zd_plan* P, int enable) {
+  if (!P) return ZD_E_INVALID_ARG;
+  if (enable && !P->ev_made) {
+    for (auto& e : P->ev) HIPCHK(hipEventCreate(&e));
+    P->ev_made = true;
+  }
+  P->profile = enable != 0;
+  return ZD_OK;
+}
+
+int zd_plan_kernel_times(zd_plan* P, const char** names, float* ms, int cap, int* n) {
+  if (!P || !P->profile || !P->launched) return ZD_E_INVALID_ARG;
+  HIPCHK(hipEventSynchronize(P->ev[N_KERNELS]));
+  int k = 0;
+  for (; k < N_KERNELS && k < cap; k++) {
+    if (names) names[k] = kKernelNames[k];
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, P->ev[k], P->ev[k + 1]));
+    if (ms) ms[k] = t;
+  }
+  if (n) *n = k;
+  return ZD_OK;
+}
+
+int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst_cap, void* stream) {
+  if (!P) return ZD_E_INVALID_ARG;
+  if (P->info.out_exact && dst_cap < P->info.out_bytes) return ZD_E_DST_TOO_SMALL;
+  hipStream_t s = (hipStream_t)stream;
+  // frame and block states are reset every launch (keys, lengths, repeat offsets, flags)
+  HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->fstate0.data(), P->fstate0.size() * sizeof(FrameState),
+                        hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
+  LaunchArgs a{};
+  a.src = d_src;
+  a.src_size = P->info.src_bytes;
+  a.out = P->info.out_exact ? d_dst : P->d_staging;
+  a.ws = P->d_ws;
+  a.W = P->W;
+  a.n_tables = (uint32_t)P->list_tables.size();
+  a.n_huf = (uint32_t)P->list_huf.size();
+  a.n_seq = (uint32_t)P->list_seq.size();
+  a.n_frames = (uint32_t)P->fdesc.size();
+  a.stream = s;
+  a.events = P->profile ? P->ev : nullptr;
+  HIPCHK(launch_pipeline(a));
+  P->launched = true;
+  return ZD_OK;
+}
+
+int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_status, uint64_t* frame_len,
+                    uint64_t* total_len, int32_t* first_error_frame) {
+  if (!P || !P->launched) return ZD_E_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipStreamSynchronize(s));
+  size_t nf = P->fdesc.size();
+  std::vector<FrameState> st(nf);
+  if (nf) HIPCHK(hipMemcpy(st.data(), P->d_ws + P->W.frame_state, nf * sizeof(FrameState), hipMemcpyDeviceToHost));
+  int first = -1;
+  int overall = 0;
+  uint64_t total = 0;
+  std::vector<uint64_t> from, to, len;
+  bool need_compact = !P->info.out_exact;
+  for (size_t f = 0; f < nf; f++) {
+    int code = key_code(st[f].key);
+    uint64_t l = st[f].out_len;
+    if (first >= 0) code = ZD_E_NOT_DECODED;
+    if (frame_status) frame_status[f] = code;
+    if (frame_len) frame_len[f] = code ? 0 : l;
+    if (code && first < 0) { first = (int)f; overall = code; }
+    if (first < 0) {
+      if (P->info.out_exact && l != P->fdesc[f].out_cap) need_compact = true;
+      from.push_back(P->fdesc[f].out);
+      to.push_back(total);
+      len.push_back(l);
+      total += l;
+    }
+  }
+  if (need_compact && !from.empty()) {
+    // exact layout but a frame came out shorter than its FCS: move through a staging copy
+    const uint8_t* stage = P->d_staging;
+    uint8_t* tmp = nullptr;
+    if (P->info.out_exact) {
+      HIPCHK(hipMalloc(&tmp, std::max<uint64_t>(P->info.out_bytes, 16)));
+      HIPCHK(hipMemcpyAsync(tmp, d_dst, P->info.out_bytes, hipMemcpyDeviceToDevice, s));
+      stage = tmp;
+    }
+    uint64_t* d_meta = nullptr;
+    size_t m = from.size();
+    HIPCHK(hipMalloc(&d_meta, 3 * m * sizeof(uint64_t)));
+    HIPCHK(hipMemcpy(d_meta, from.data(), m * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_meta + m, to.data(), m * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_meta + 2 * m, len.data(), m * 8, hipMemcpyHostToDevice));
+    HIPCHK(launch_compact(stage, d_dst, d_meta, d_meta + m, d_meta + 2 * m, (uint32_t)m, s));
+    HIPCHK(hipStreamSynchronize(s));
+    (void)hipFree(d_meta);
+    if (tmp) (void)hipFree(tmp);
+  }
+  if (first < 0 && P->index_status) { first = (int)nf; overall = P->index_status; }
+  if (total_len) *total_len = total;
+  if (first_error_frame) *first_error_frame = first;
+  return overall;
+}
+
+int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, uint32_t flags) {
+  zd_plan* P = nullptr;
+  int r = zd_plan_create(src, n, flags, &P);
+  if (r) return r;
+  uint8_t *d_src = nullptr, *d_dst = nullptr;
+  uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
+  auto cleanup = [&]() { if (d_src) (void)hipFree(d_src); if (d_dst) (void)hipFree(d_dst); zd_plan_destroy(P); };
+  if (hipMalloc(&d_src, std::max<size_t>(n, 16)) != hipSuccess || hipMalloc(&d_dst, ob) != hipSuccess) {
+    cleanup(); return ZD_E_HIP;
+  }
+  if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) { cleanup(); return ZD_E_HIP; }
+  r = zd_decode_async(P, d_src, d_dst, ob, nullptr);
+  uint64_t total = 0;
+  int32_t first = -1;
+  if (!r) r = zd_plan_results(P, d_dst, nullptr, nullptr, nullptr, &total, &first);
+  if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG) { cleanup(); return r; }
+  int status = r;
+  size_t copy = (size_t)std::min<uint64_t>(total, cap);
+  if (copy && dst && hipMemcpy(dst, d_dst, copy, hipMemcpyDeviceToHost) != hipSuccess) { cleanup(); return ZD_E_HIP; }
+  if (out_len) *out_len = (size_t)total;
+  cleanup();
+  if (!status && total > cap) return ZD_E_DST_TOO_SMALL;
+  return status;
+}
+
+// ===========================================================================
+// DecodingContext mirror
+// ===========================================================================
+}  // extern "C"
+
+struct zd_context {
+  uint64_t window = 0;
+  uint8_t* d_out = nullptr;     // decoded (capacity d_cap)
+  uint64_t d_cap = 0;
+  uint64_t len = 0;
+  uint64_t rep[3] = {1, 4, 8};
+  // persisted tables of the previous blocks (one virtual comp block)
+  uint16_t* d_lut = nullptr;    // LUT_ENTRIES
+  uint32_t* d_fse = nullptr;    // 3 * FSE_ENTRIES
+  uint8_t huf_bits = 0;
+  uint8_t al[3] = {0, 0, 0};
+  bool has_huf = false;
+  bool has_tab[3] = {false, false, false};
+};
+
+namespace {
+
+int ctx_reserve(zd_context* c, uint64_t need) {
+  if (need <= c->d_cap) return 0;
+  uint64_t nc = std::max<uint64_t>(c->d_cap ? c->d_cap * 2 : (1 << 20), need);
+  uint8_t* nd = nullptr;
+  HIPCHK(hipMalloc(&nd, nc));
+  if (c->len) HIPCHK(hipMemcpy(nd, c->d_out, c->len, hipMemcpyDeviceToDevice));
+  if (c->d_out) (void)hipFree(c->d_out);
+  c->d_out = nd;
+  c->d_cap = nc;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int zd_context_new(uint64_t window_size, zd_context** out) {
+  if (!out) return ZD_E_INVALID_ARG;
+  if (window_size > MAX_WIN_SIZE) return ZD_E_CTX_WINDOW_SIZE_TOO_BIG;   // decoding_context.rs:29-35
+  zd_context* c = new (std::nothrow) zd_context();
+  if (!c) return ZD_E_NO_MEMORY;
+  c->window = window_size;
+  if (hipMalloc(&c->d_lut, LUT_ENTRIES * 2) != hipSuccess || hipMalloc(&c->d_fse, 3 * FSE_ENTRIES * 4) != hipSuccess) {
+    zd_context_free(c);
+    return ZD_E_HIP;
+  }
+  *out = c;
+  return ZD_OK;
+}
+
+void zd_context_free(zd_context* c) {
+  if (!c) return;
+  if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_lut) (void)hipFree(c->d_lut);
+  if (c->d_fse) (void)hipFree(c->d_fse);
+  delete c;
+}
+
+int zd_context_decoded(const zd_context* c, uint8_t* dst, size_t cap, size_t* len) {
+  if (!c) return ZD_E_INVALID_ARG;
+  if (len) *len = c->len;
+  size_t k = (size_t)std::min<uint64_t>(cap, c->len);
+  if (k && dst) HIPCHK(hipMemcpy(dst, c->d_out, k, hipMemcpyDeviceToHost));
+  return cap < c->len ? ZD_E_DST_TOO_SMALL : ZD_OK;
+}
+
+int zd_context_offsets(const zd_context* c, uint64_t offsets[3]) {
+  if (!c || !offsets) return ZD_E_INVALID_ARG;
+  for (int i = 0; i < 3; i++) offsets[i] = c->rep[i];
+  return ZD_OK;
+}
+
+// Runs a one-frame plan whose output continues the context's decoded buffer.
+static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
+  uint8_t* d_src = nullptr;
+  auto fin = [&](int r) { if (d_src) (void)hipFree(d_src); return r; };
+  if (hipMalloc(&d_src, std::max<size_t>(n, 16)) != hipSuccess) return ZD_E_HIP;
+  if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+  if (int r = upload_plan(P)) return fin(r);
+  HIPCHK(hipMemset(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState)));
+  // prebuilt comp 0 carries the context's tables
+  if (P->has_prebuilt) {
+    const CompBlock& pb = P->comps[0];
+    uint8_t* luts = P->d_ws + P->W.luts + (uint64_t)pb.lut_slot * LUT_ENTRIES * 2;
+    uint8_t* fses = P->d_ws + P->W.fses + (uint64_t)pb.fse_slot * FSE_ENTRIES * 4 * 3;
+    if (hipMemcpy(luts, c->d_lut, LUT_ENTRIES * 2, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
+    if (hipMemcpy(fses, c->d_fse, 3 * FSE_ENTRIES * 4, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
+    CompState cs{};
+    cs.huf_bits = c->huf_bits;
+    for (int k = 0; k < 3; k++) cs.al[k] = c->al[k];
+    if (hipMemcpy(P->d_ws + P->W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+  }
+  P->info.out_exact = 1;    // output goes straight into the context buffer
+  P->fdesc[0].out = 0;
+  if (hipMemcpy(P->d_ws + P->W.frames, P->fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice) != hipSuccess)
+    return fin(ZD_E_HIP);
+  HIPCHK(hipMemcpy(P->d_ws + P->W.frame_state, P->fstate0.data(), sizeof(FrameState), hipMemcpyHostToDevice));
+  LaunchArgs a{};
+  a.src = d_src; a.src_size = n; a.out = c->d_out; a.ws = P->d_ws; a.W = P->W;
+  a.n_tables = (uint32_t)P->list_tables.size();
+  a.n_huf = (uint32_t)P->list_huf.size();
+  a.n_seq = (uint32_t)P->list_seq.size();
+  a.n_frames = 1;
+  a.stream = nullptr;
+  if (launch_pipeline(a) != hipSuccess) return fin(ZD_E_HIP);
+  if (hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
+  FrameState st{};
+  if (hipMemcpy(&st, P->d_ws + P->W.frame_state, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return fin(ZD_E_HIP);
+  int code = key_code(st.key);
+  if (code) return fin(code);
+  c->len = st.out_len;
+  for (int i = 0; i < 3; i++) c->rep[i] = st.rep[i];
+  // persist tables defined by the real block (comp index 1 when prebuilt, else 0)
+  size_t ci = P->has_prebuilt ? 1 : 0;
+  if (ci < P->comps.size()) {
+    const CompBlock& cb = P->comps[ci];
+    CompState cs{};
+    if (hipMemcpy(&cs, P->d_ws + P->W.comp_state + ci * sizeof(CompState), sizeof cs, hipMemcpyDeviceToHost) != hipSuccess)
+      return fin(ZD_E_HIP);
+    if (cb.lit_type == LIT_COMPRESSED) {
+      if (hipMemcpy(c->d_lut, P->d_ws + P->W.luts + (uint64_t)cb.lut_slot * LUT_ENTRIES * 2, LUT_ENTRIES * 2,
+                    hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
+      c->huf_bits = cs.huf_bits;
+      c->has_huf = true;
+    }
+    for (int k = 0; k < 3 && cb.nseq; k++) {
+      int32_t srcc = cb.tab_src[k];
+      if (srcc < 0) continue;
+      const CompBlock& sb = P->comps[(size_t)srcc];
+      CompState ss{};
+      if (hipMemcpy(&ss, P->d_ws + P->W.comp_state + (size_t)srcc * sizeof(CompState), sizeof ss, hipMemcpyDeviceToHost) != hipSuccess)
+        return fin(ZD_E_HIP);
+      if ((size_t)srcc == ci) {
+        if (hipMemcpy(c->d_fse + k * FSE_ENTRIES,
+                      P->d_ws + P->W.fses + ((uint64_t)sb.fse_slot * 3 + k) * FSE_ENTRIES * 4, FSE_ENTRIES * 4,
+                      hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
+        c->al[k] = ss.al[k];
+      }
+      c->has_tab[k] = true;
+    }
+  }
+  return fin(ZD_OK);
+}
+
+int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consumed, int* last) {
+  if (!c || (!src && n)) return ZD_E_INVALID_ARG;
+  // Block::parse (block.rs:43-72) on the host side
+  Bytes in{src, n};
+  const uint8_t* h;
+  if (int r = in.slice(3, &h)) return r;
+  uint32_t x = h[0] | (h[1] << 8) | ((uint32_t)h[2] << 16);
+  HostBlock hb;
+  memset(&hb, 0, sizeof hb);
+  hb.last = x & 1; hb.type = (x >> 1) & 3; hb.size = x >> 3; hb.src = 3;
+  if (hb.type == 0) { const uint8_t* s; if (int r = in.slice(hb.size, &s)) return r; }
+  else if (hb.type == 1) { if (int r = in.u8(&hb.rle)) return r; }
+  else if (hb.type == 2) {
+    const uint8_t* s;
+    if (int r = in.slice(hb.size, &s)) return r;
+    hb.cb.src = 3; hb.cb.size = hb.size; hb.cb.host_stage = PS_ALL;
+    Err e;
+    if (int r = parse_compressed(src, 3, hb.size, &hb.cb, &e)) return r;
+  } else return ZD_E_RESERVED_BLOCK_TYPE;
+  size_t used = n - in.n;
+  if (consumed) *consumed = used;
+  if (last) *last = hb.last;
+
+  zd_plan P;
+  HostFrame hf;
+  memset(&hf.d, 0, sizeof hf.d);
+  hf.d.kind = ZD_FRAME_ZSTD;
+  hf.d.content_size = UINT64_MAX;
+  int32_t prev_huf = -1, prev_tab[3] = {-1, -1, -1};
+  bool need_pre = c->has_huf || c->has_tab[0] || c->has_tab[1] || c->has_tab[2];
+  if (need_pre) {
+    // virtual previous block: a compressed block that is never decoded
+    HostBlock pre;
+    memset(&pre, 0, sizeof pre);
+    pre.type = 2;
+    pre.cb.lit_type = LIT_COMPRESSED;
+    pre.cb.host_stage = PS_ALL;
+    pre.cb.nseq = 1;
+    pre.cb.modes[0] = pre.cb.modes[1] = pre.cb.modes[2] = M_FSE;
+    hf.blocks.push_back(pre);
+    P.has_prebuilt = true;
+    if (c->has_huf) prev_huf = 0;
+    for (int k = 0; k < 3; k++) if (c->has_tab[k]) prev_tab[k] = 0;
+  }
+  hf.blocks.push_back(hb);
+  P.frames.push_back(hf);
+  // resolve with the prebuilt block as "previous": build_plan walks the blocks in
+  // order, so the virtual block seeds Treeless/Repeat through prev_huf/prev_tab.
+  uint64_t cap = c->len + (hb.type == 2 ? (uint64_t)MAX_BLOCK_OUT : (uint64_t)hb.size);
+  if (int r = ctx_reserve(c, cap + 16)) return r;
+  uint64_t rep0[3] = {c->rep[0], c->rep[1], c->rep[2]};
+  build_plan(&P, prev_huf, prev_tab, c->len, rep0, c->d_cap);
+  if (P.has_prebuilt) {
+    // the virtual block: prebuilt, never executed, tables self-referencing
+    CompBlock& pb = P.comps[0];
+    pb.prebuilt = 1;
+    pb.huf_src = 0;
+    for (int k = 0; k < 3; k++) pb.tab_src[k] = 0;
+    P.list_tables.erase(std::remove(P.list_tables.begin(), P.list_tables.end(), 0u), P.list_tables.end());
+    P.list_huf.erase(std::remove(P.list_huf.begin(), P.list_huf.end(), 0u), P.list_huf.end());
+    P.list_seq.erase(std::remove(P.list_seq.begin(), P.list_seq.end(), 0u), P.list_seq.end());
+    // the real block resolves Treeless/Repeat against comp 0 (build_plan already
+    // chained them through the virtual block's own FSE/Compressed modes)
+    P.blocks[0].type = 5;    // skip in execute
+    FrameState& fs = P.fstate0[0];
+    fs.key = KEY_NONE;
+    // re-derive host decode errors for the real block only
+    CompBlock& cb = P.comps[1];
+    if (cb.lit_type == LIT_TREELESS && !c->has_huf)
+      fs.key = std::min(fs.key, make_key(PH_DECODE, 1, DS_LITERALS, 0, ZD_E_HUFFMAN_DECODER_MISSING));
+    if (cb.nseq == 0) {
+      int code = ZD_E_EMPTY_INPUT_DATA;
+      for (int k = 0; k < 3; k++) if (!c->has_tab[k]) { code = ZD_E_NO_PREVIOUS_DECODER; break; }
+      fs.key = std::min(fs.key, make_key(PH_DECODE, 1, DS_SEQUENCES, 0, code));
+    } else {
+      for (int k = 0; k < 3; k++) {
+        if (cb.modes[k] == M_REPEAT) {
+          if (!c->has_tab[k]) {
+            fs.key = std::min(fs.key, make_key(PH_DECODE, 1, DS_SEQUENCES, 0, ZD_E_NO_PREVIOUS_DECODER));
+            cb.tab_src[k] = -1;
+            break;
+          }
+          cb.tab_src[k] = 0;
+        }
+      }
+      bool ok = cb.tab_src[0] >= 0 && cb.tab_src[1] >= 0 && cb.tab_src[2] >= 0;
+      P.list_seq.erase(std::remove(P.list_seq.begin(), P.list_seq.end(), 1u), P.list_seq.end());
+      if (ok) P.list_seq.push_back(1);
+    }
+    if (cb.lit_type == LIT_TREELESS) {
+      cb.huf_src = c->has_huf ? 0 : -1;
+      P.list_huf.erase(std::remove(P.list_huf.begin(), P.list_huf.end(), 1u), P.list_huf.end());
+      if (cb.huf_src >= 0 && cb.nstreams) P.list_huf.push_back(1);
+    }
+  }
+  P.info.src_bytes = n;
+  int r = ctx_run(c, &P, src, n);
+  if (P.d_ws) { (void)hipFree(P.d_ws); P.d_ws = nullptr; }
+  if (P.d_staging) { (void)hipFree(P.d_staging); P.d_staging = nullptr; }
+  return r;
+}
+
+int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv, const uint32_t* ml, size_t nseq,
+                         const uint8_t* lits, size_t nlits) {
+  if (!c || (nseq && (!ll || !ofv || !ml)) || (nlits && !lits)) return ZD_E_INVALID_ARG;
+  // One synthetic compressed block whose literals are raw (taken from `lits`)
+  // and whose sequences are pre-decoded: only the execute kernel runs.
+  uint64_t need = c->len + nlits;
+  for (size_t i = 0; i < nseq; i++) need += ml[i];
+  if (int r = ctx_reserve(c, need + 16)) return r;
+  zd_plan P;
+  HostFrame hf;
+  memset(&hf.d, 0, sizeof hf.d);
+  hf.d.kind = ZD_FRAME_ZSTD;
+  hf.d.content_size = UINT64_MAX;
+  HostBlock hb;
+  memset(&hb, 0, sizeof hb);
+  hb.type = 2; hb.size = (uint32_t)nlits; hb.src = 0; hb.last = 1;
+  hb.cb.lit_type = LIT_RAW; hb.cb.lit_regen = (uint32_t)nlits; hb.cb.lit_data = 0;
+  hb.cb.nseq = (uint32_t)nseq; hb.cb.host_stage = PS_ALL;
+  hb.cb.modes[0] = hb.cb.modes[1] = hb.cb.modes[2] = M_RLE;
+  hf.blocks.push_back(hb);
+  P.frames.push_back(hf);
+  int32_t none[3] = {-1, -1, -1};
+  uint64_t rep0[3] = {c->rep[0], c->rep[1], c->rep[2]};
+  build_plan(&P, -1, none, c->len, rep0, c->d_cap);
+  P.list_tables.clear();
+  P.list_huf.clear();
+  P.list_seq.clear();   // sequences come from the caller
+  P.info.src_bytes = nlits;
+  uint8_t* d_src = nullptr;
+  int r = upload_plan(&P);
+  auto fin = [&](int rr) {
+    if (d_src) (void)hipFree(d_src);
+    if (P.d_ws) (void)hipFree(P.d_ws);
+    if (P.d_staging) (void)hipFree(P.d_staging);
+    P.d_ws = nullptr; P.d_staging = nullptr;
+    return rr;
+  };
+  if (r) return fin(r);
+  if (hipMalloc(&d_src, std::max<size_t>(nlits, 16)) != hipSuccess) return fin(ZD_E_HIP);
+  if (nlits && hipMemcpy(d_src, lits, nlits, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+  if (nseq) {
+    if (hipMemcpy(P.d_ws + P.W.seq_ll, ll, nseq * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(P.d_ws + P.W.seq_of, ofv, nseq * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(P.d_ws + P.W.seq_ml, ml, nseq * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return fin(ZD_E_HIP);
+  }
+  CompState cs{};
+  cs.lit_count = (uint32_t)nlits;
+  if (hipMemcpy(P.d_ws + P.W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+  P.fdesc[0].out = 0;
+  if (hipMemcpy(P.d_ws + P.W.frames, P.fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice) != hipSuccess)
+    return fin(ZD_E_HIP);
+  if (hipMemcpy(P.d_ws + P.W.frame_state, P.fstate0.data(), sizeof(FrameState), hipMemcpyHostToDevice) != hipSuccess)
+    return fin(ZD_E_HIP);
+  LaunchArgs a{};
+  a.src = d_src; a.src_size = nlits; a.out = c->d_out; a.ws = P.d_ws; a.W = P.W;
+  a.n_frames = 1;
+  if (launch_pipeline(a) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
+  FrameState st{};
+  if (hipMemcpy(&st, P.d_ws + P.W.frame_state, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return fin(ZD_E_HIP);
+  int code = key_code(st.key);
+  if (code) return fin(code);
+  c->len = st.out_len;
+  for (int i = 0; i < 3; i++) c->rep[i] = st.rep[i];
+  return fin(ZD_OK);
+}
+
+}  // extern "C"

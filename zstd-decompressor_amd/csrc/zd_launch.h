@@ -1,0 +1,31 @@
+// zd_launch.h — host-side entry points of the gfx950 kernels (zd_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zd_common.h"
+
+namespace zd {
+
+struct LaunchArgs {
+  const uint8_t* src;      // d_src
+  uint64_t src_size;
+  uint8_t* out;            // output base (d_dst or the plan's staging buffer)
+  uint8_t* ws;             // workspace base
+  Workspace W;
+  uint32_t n_tables, n_huf, n_seq, n_frames;
+  hipStream_t stream;
+  hipEvent_t* events;      // optional: 5 events recorded around the 4 kernels
+};
+
+// K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
+hipError_t launch_pipeline(const LaunchArgs& a);
+
+// Copies frame outputs from staging (at cap offsets) to exact offsets.
+hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* d_from,
+                          const uint64_t* d_to, const uint64_t* d_len, uint32_t n, hipStream_t s);
+
+constexpr int N_KERNELS = 4;
+extern const char* const kKernelNames[N_KERNELS];
+
+}  // namespace zd

@@ -1,0 +1,109 @@
+"""Batch decode over the C ABI — the hot path.
+
+`decompress` mirrors the CLI loop (src/main.rs:43-58) on host buffers;
+`Plan` keeps input/output in HBM (torch tensors or raw device pointers) and is
+what bench.py times.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _lib
+from ._lib import ZdError, FrameDesc, BlockDesc, PlanInfo
+
+
+def frames_index(data: bytes, max_frames: int = 0):
+    """zd_frames_index: ([frame dicts], [block dicts], status, consumed)."""
+    L = _lib.lib()
+    p, n, keep = _lib.buf(data)
+    nf, nb, cons = C.c_size_t(), C.c_size_t(), C.c_size_t()
+    L.zd_frames_index(p, n, None, 0, C.byref(nf), None, 0, C.byref(nb), C.byref(cons))
+    fa = (FrameDesc * max(nf.value, 1))()
+    ba = (BlockDesc * max(nb.value, 1))()
+    st = L.zd_frames_index(p, n, fa, nf.value, C.byref(nf), ba, nb.value, C.byref(nb), C.byref(cons))
+    frames = [{k: getattr(fa[i], k) for k, _ in FrameDesc._fields_} for i in range(nf.value)]
+    blocks = [{k: getattr(ba[i], k) for k, _ in BlockDesc._fields_ if k != "_pad"} for i in range(nb.value)]
+    return frames, blocks, st, cons.value
+
+
+def decompress(data: bytes, print_skippable: bool = False) -> bytes:
+    """Decode every frame of `data` on the GPU (host in, host out)."""
+    L = _lib.lib()
+    p, n, keep = _lib.buf(data)
+    # size the output from the plan (exact when every frame carries its FCS)
+    plan = Plan(data, print_skippable)
+    cap = max(plan.info.out_bytes, 1)
+    plan.close()
+    out = (C.c_uint8 * cap)()
+    ol = C.c_size_t()
+    st = L.zd_decompress(p, n, out, cap, C.byref(ol), _lib.F_SKIPPABLE if print_skippable else 0)
+    _lib.check(st, "zd_decompress")
+    return bytes(out[: ol.value])
+
+
+def decompress_status(data: bytes, print_skippable: bool = False):
+    """(status, output of the frames before the first failure)."""
+    L = _lib.lib()
+    p, n, keep = _lib.buf(data)
+    plan = Plan(data, print_skippable)
+    cap = max(plan.info.out_bytes, 1)
+    plan.close()
+    out = (C.c_uint8 * cap)()
+    ol = C.c_size_t()
+    st = L.zd_decompress(p, n, out, cap, C.byref(ol), _lib.F_SKIPPABLE if print_skippable else 0)
+    if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
+        _lib.check(st, "zd_decompress")
+    return st, bytes(out[: min(ol.value, cap)])
+
+
+class Plan:
+    """zd_plan: host index + device workspace for one byte range of frames."""
+
+    def __init__(self, data: bytes, print_skippable: bool = False):
+        L = _lib.lib()
+        self._data = data
+        p, n, self._keep = _lib.buf(data)
+        h = C.c_void_p()
+        _lib.check(L.zd_plan_create(p, n, _lib.F_SKIPPABLE if print_skippable else 0, C.byref(h)), "zd_plan_create")
+        self._h = h
+        self.info = PlanInfo()
+        _lib.check(L.zd_plan_info_get(h, C.byref(self.info)), "zd_plan_info_get")
+
+    def set_profiling(self, on: bool = True):
+        _lib.check(_lib.lib().zd_plan_set_profiling(self._h, int(on)))
+
+    def decode_async(self, d_src: int, d_dst: int, dst_cap: int, stream: int = 0):
+        """Launch the pipeline; pointers/stream are integers (e.g. tensor.data_ptr(),
+        torch.cuda.current_stream().cuda_stream)."""
+        _lib.check(_lib.lib().zd_decode_async(self._h, C.c_void_p(d_src), C.c_void_p(d_dst), dst_cap,
+                                              C.c_void_p(stream)), "zd_decode_async")
+
+    def results(self, d_dst: int, stream: int = 0):
+        """(status, total_len, per-frame statuses, per-frame lengths, first error frame)."""
+        nf = self.info.nframes
+        st_arr = (C.c_int32 * max(nf, 1))()
+        ln_arr = (C.c_uint64 * max(nf, 1))()
+        total, first = C.c_uint64(), C.c_int32()
+        st = _lib.lib().zd_plan_results(self._h, C.c_void_p(d_dst), C.c_void_p(stream), st_arr, ln_arr,
+                                        C.byref(total), C.byref(first))
+        if st in (_lib.HIP, _lib.INVALID_ARG):
+            _lib.check(st, "zd_plan_results")
+        return st, total.value, list(st_arr)[:nf], list(ln_arr)[:nf], first.value
+
+    def kernel_times(self):
+        names = (C.c_char_p * 8)()
+        ms = (C.c_float * 8)()
+        n = C.c_int()
+        _lib.check(_lib.lib().zd_plan_kernel_times(self._h, names, ms, 8, C.byref(n)))
+        return {names[i].decode(): ms[i] for i in range(n.value)}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().zd_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

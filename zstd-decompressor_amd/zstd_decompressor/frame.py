@@ -1,0 +1,108 @@
+"""Frame layer (frame.rs): Frame, ZStandard, Skippable, Header, FrameIterator.
+
+Frame.parse runs the host index (zd_frames_index: FrameIterator/Frame::parse/
+Header::parse/Block::parse structure, frame.rs:61-230); Frame.decode runs the
+HIP pipeline (zd_decompress) — ZStandard::decode (frame.rs:232-260).
+Differences from the Rust API: entropy-table errors that the reference raises
+inside Frame::parse (Huffman/FSE descriptions) are raised by decode(), which
+is where the GPU parses those tables.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _lib
+from ._lib import ZdError, FrameDesc, BlockDesc
+
+MAGIC_ZSTD = 0xFD2FB528           # frame.rs:41
+MAGIC_SKIP = 0x184D2A50           # frame.rs:42
+MAX_WIN_SIZE = 8 << 20            # frame.rs:44
+_NONE = (1 << 64) - 1
+
+
+class Header:                     # frame.rs:103-108
+    def __init__(self, d: FrameDesc):
+        self.content_checksum_flag = bool(d.has_checksum)
+        self.window_size = d.window_size
+        self.dictionnary_id = None if d.dict_id == _NONE else d.dict_id
+        self.content_size = None if d.content_size == _NONE else d.content_size
+
+    def __repr__(self):
+        return (f"Header(content_checksum_flag={self.content_checksum_flag}, window_size={self.window_size}, "
+                f"dictionnary_id={self.dictionnary_id}, content_size={self.content_size})")
+
+
+class Skippable:                  # frame.rs:55-58
+    def __init__(self, magic: int, data: bytes):
+        self.magic, self.data = magic, data
+
+    def decode(self) -> bytes:
+        return bytes(self.data)
+
+
+class ZStandard:                  # frame.rs:189-272
+    def __init__(self, raw: bytes, d: FrameDesc, blocks):
+        self._raw, self._d, self._blocks = raw, d, blocks
+        self._header = Header(d)
+
+    def header(self) -> Header:
+        return self._header
+
+    def checksum(self):
+        return self._d.checksum if self._d.has_checksum else None
+
+    def blocks(self):
+        return self._blocks
+
+    def decode(self) -> bytes:
+        from .batch import decompress
+        return decompress(self._raw)
+
+
+class Frame:
+    """Frame::ZStandardFrame / Frame::SkippableFrame (frame.rs:48-84)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+
+    @property
+    def is_skippable(self) -> bool:
+        return isinstance(self.inner, Skippable)
+
+    @staticmethod
+    def parse(parser) -> "Frame":
+        L = _lib.lib()
+        data = parser.remaining()
+        p, n, keep = _lib.buf(data)
+        fa = (FrameDesc * 1)()
+        nf, nb, cons = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        # first pass: block count of the first frame
+        st = L.zd_frames_index(p, n, fa, 1, C.byref(nf), None, 0, C.byref(nb), C.byref(cons))
+        if st != 0 and nf.value == 0:
+            raise ZdError(st, "Frame::parse")
+        ba = (BlockDesc * max(nb.value, 1))()
+        L.zd_frames_index(p, n, fa, 1, C.byref(nf), ba, nb.value, C.byref(nb), C.byref(cons))
+        d = fa[0]
+        raw = data[d.src_offset:d.src_offset + d.src_size]
+        parser.advance(d.src_offset + d.src_size)
+        if d.kind == 1:
+            return Frame(Skippable(d.magic, raw[8:]))
+        from .block import Block
+        blocks = [Block._from_desc(raw, ba[i], d.src_offset) for i in range(nb.value)]
+        return Frame(ZStandard(raw, d, blocks))
+
+    def decode(self) -> bytes:
+        return self.inner.decode()
+
+
+class FrameIterator:              # frame.rs:86-99
+    def __init__(self, parser):
+        self.parser = parser
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> Frame:
+        if self.parser.is_empty():
+            raise StopIteration
+        return Frame.parse(self.parser)
