@@ -67,10 +67,11 @@ def test_context_block_by_block(resources):
     _, expect, _ = oracle.frame_decode(data)
     p = ForwardByteParser(data)
     p.slice(4)                                     # magic
-    fhd = p.u8()
-    assert fhd & 0x20 == 0                         # not single segment: window descriptor
-    p.u8()
-    fcs_len = {0: 0, 1: 2, 2: 4, 3: 8}[fhd >> 6]
+    fhd = p.u8()                                   # Header::parse (frame.rs:111-177)
+    single = bool(fhd & 0x20)
+    if not single:
+        p.u8()                                     # window descriptor
+    fcs_len = {0: 1 if single else 0, 1: 2, 2: 4, 3: 8}[fhd >> 6]
     if fcs_len:
         p.slice(fcs_len)
     ctx = DecodingContext(MAX_WIN_SIZE)

@@ -426,7 +426,8 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     fd.nblocks = (uint32_t)hf.blocks.size();
     uint64_t cap;
     if (hf.d.kind == ZD_FRAME_SKIPPABLE) {
-      cap = (P->flags & ZD_F_SKIPPABLE) ? hf.blocks[0].size : 0;
+      // a truncated skippable frame fails to index and keeps no payload block
+      cap = ((P->flags & ZD_F_SKIPPABLE) && !hf.blocks.empty()) ? hf.blocks[0].size : 0;
       if (!(P->flags & ZD_F_SKIPPABLE)) fd.nblocks = 0;
     } else if (hf.d.content_size != UINT64_MAX && hf.d.content_size <= bound) {
       cap = hf.d.content_size;
