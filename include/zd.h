@@ -159,8 +159,14 @@ int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out);
 int zd_plan_info_get(const zd_plan* plan, zd_plan_info* info);
 void zd_plan_destroy(zd_plan* plan);
 
+/* Bitstream readers fetch aligned 16-byte windows and may touch up to
+ * ZD_SRC_PADDING bytes past the end of the input: device input buffers must
+ * stay readable that far (the contents there do not matter). */
+#define ZD_SRC_PADDING 16
+
 /* Launch the decode pipeline on `stream`.  d_src holds the same n bytes
- * given to zd_plan_create, resident in HBM; d_dst receives the
+ * given to zd_plan_create, resident in HBM (readable for n + ZD_SRC_PADDING
+ * bytes); d_dst receives the
  * concatenated output (>= info.out_bytes).  No host synchronisation, no
  * allocation: safe to capture in a hipGraph. */
 int zd_decode_async(zd_plan* plan, const uint8_t* d_src, uint8_t* d_dst,

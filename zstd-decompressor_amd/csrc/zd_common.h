@@ -23,8 +23,123 @@ constexpr uint32_t MAX_BLOCK_OUT = 128u << 10;   // RFC Block_Maximum_Size (capa
 // LUT entry: symbol | nbits << 8 | ABSENT (depth of the absent tree node in nbits)
 constexpr uint16_t LUT_ABSENT = 0x8000;
 
-// FSE decode entry: symbol | nbits << 8 | baseline << 16
-ZD_HD inline uint32_t fse_entry(uint32_t sym, uint32_t nb, uint32_t base) { return sym | (nb << 8) | (base << 16); }
+// FSE decode entry, 16 bits: symbol (clamped to 63) | nextState << 6.
+// FseTable::from_distribution (fse.rs:169-189) gives state u of symbol s
+// nextState ns = count(s) + u in [1, 2T); the reference's {bits_to_read,
+// baseline} are recovered as nb = AL - highbit(ns), base = (ns << nb) - T.
+// Every sequence code above 63 is already past LL/ML/OF maxima (35/52/31) and
+// every Huffman weight above 32 already panics, so the clamp keeps behaviour.
+constexpr int FSE_TAB = 1 << FSE_MAX_AL;           // u16 entries per table in a slot
+constexpr int FSE_SLOT = 3 * FSE_TAB;              // LL | OF | ML
+ZD_HD inline uint16_t fse_entry(uint32_t sym, uint32_t ns) { return (uint16_t)((sym > 63 ? 63 : sym) | (ns << 6)); }
+ZD_HD inline int hb32(uint32_t v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return 31 - __clz(v);
+#else
+  return 31 - __builtin_clz(v);
+#endif
+}
+ZD_HD inline uint32_t fse_sym(uint16_t e) { return e & 63; }
+ZD_HD inline uint32_t fse_nb(uint16_t e, int al) { return (uint32_t)(al - hb32((uint32_t)e >> 6)); }
+ZD_HD inline uint32_t fse_base(uint16_t e, int al) {
+  uint32_t ns = (uint32_t)e >> 6;
+  return (ns << fse_nb(e, al)) - (1u << al);
+}
+
+// Sequence codes -> (baseline, extra bits) (decoders/sequence.rs:98-191) as
+// arithmetic instead of the reference's linear table search (sequence.rs:36).
+// Offsets 16..24 (LL) / 32..42 (ML) above the base: 0,2,4,6 then
+// (2 + odd) << (k >> 1).
+ZD_HD inline uint32_t code_step(uint32_t k) {
+  return ((2u + (k & 1)) << ((k >> 1) & 31)) - (k < 2 ? 2 - k : 0);
+}
+// (branch-free: selects, no divergent control flow in the per-lane decoders)
+ZD_HD inline void ll_code(uint32_t c, uint32_t* base, uint32_t* bits) {
+  const uint32_t k = (c - 16) & 15, hi = (c - 19) & 31;
+  const uint32_t mb = k < 2 ? 1 : (k >> 1), mbase = 16 + code_step(k);
+  *bits = c < 16 ? 0 : (c < 25 ? mb : hi);
+  *base = c < 16 ? c : (c < 25 ? mbase : (1u << hi));
+}
+ZD_HD inline void ml_code(uint32_t c, uint32_t* base, uint32_t* bits) {
+  const uint32_t k = (c - 32) & 15, hi = (c - 36) & 31;
+  const uint32_t mb = k < 2 ? 1 : (k >> 1), mbase = 35 + code_step(k);
+  *bits = c < 32 ? 0 : (c < 43 ? mb : hi);
+  *base = c < 32 ? c + 3 : (c < 43 ? mbase : (1u << hi) + 3);
+}
+
+// ---------------------------------------------------------------------------
+// Decoded sequence record (K3 -> K4), 8 bytes:
+//   bits 0-16 literals_length (<= 131071), 17-34 match_length (<= 131074),
+//   35-63 offset code.
+// The offset code is DecodingContext::decode_offset (decoding_context.rs:
+// 50-75) evaluated per block against a *symbolic* incoming repeat state, so
+// blocks decode in parallel; K4 resolves it against the real state:
+//   v <  OFF_SYM                    concrete offset v
+//   OFF_SYM + (slot << 24) + d      incoming rep[slot] - d (d decrements of
+//                                   the `3, ll == 0` rule; underflow when
+//                                   rep[slot] < d: the reference panics)
+//   OFF_GIANT                       an offset >= 2^28: past any frame the GPU
+//                                   path accepts (ImpossibleValue)
+//   OFF_NULL                        offset_value 0 (NullOffsetError)
+//   OFF_UNDERFLOW                   usize underflow of rep0 - 1 (ZD_E_REF_PANIC)
+// ---------------------------------------------------------------------------
+constexpr uint32_t OFF_SYM = 1u << 28;
+constexpr uint32_t OFF_GIANT = (1u << 29) - 3;
+constexpr uint32_t OFF_NULL = (1u << 29) - 2;
+constexpr uint32_t OFF_UNDERFLOW = (1u << 29) - 1;
+constexpr uint64_t MAX_FRAME_OUT = 1ull << 27;   // frames the GPU path decodes (OFF_GIANT stays impossible)
+
+ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t offc) {
+  return (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)offc << 35);
+}
+ZD_HD inline uint32_t seq_ll(uint64_t s) { return (uint32_t)(s & 0x1FFFF); }
+ZD_HD inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >> 17) & 0x3FFFF); }
+ZD_HD inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 35); }
+
+ZD_HD inline void rep_init(uint32_t r[3]) { r[0] = OFF_SYM; r[1] = OFF_SYM | (1u << 24); r[2] = OFF_SYM | (2u << 24); }
+ZD_HD inline uint32_t rep_dec1(uint32_t v) {
+  // giant stays giant; after an underflow the reference stopped; a symbolic
+  // value counts one more decrement; 0 underflows.  Written as a chain of
+  // selects (no divergent branches in the per-lane decoder).
+  uint32_t t = v >= OFF_SYM ? v + 1 : v - 1;
+  t = v == 0 ? OFF_UNDERFLOW : t;
+  return v >= OFF_GIANT ? v : t;
+}
+// decode_offset (decoding_context.rs:50-75) on codes; returns the offset code.
+// idx = the repeat slot an offset_value <= 3 names (RFC 8878 3.1.1.5), 3
+// being `rep0 - 1`.
+ZD_HD inline uint32_t rep_step(uint32_t r[3], uint32_t ofv, uint32_t ll) {
+  const uint32_t r0 = r[0], r1 = r[1], r2 = r[2];
+  const bool fresh = ofv > 3;
+  const uint32_t idx = ofv - (ll != 0 ? 1u : 0u);
+  uint32_t rep = idx == 0 ? r0 : r1;
+  rep = idx >= 2 ? r2 : rep;
+  rep = idx == 3 ? rep_dec1(r0) : rep;
+  const uint32_t v = ofv - 3;
+  const uint32_t n0 = fresh ? (v >= OFF_SYM ? OFF_GIANT : v) : rep;
+  const uint32_t n1 = (!fresh && idx == 0) ? r1 : r0;
+  const uint32_t n2 = (!fresh && idx <= 1) ? r2 : r1;
+  const bool null = ofv == 0;
+  r[0] = null ? r0 : n0;
+  r[1] = null ? r1 : n1;
+  r[2] = null ? r2 : n2;
+  return null ? OFF_NULL : n0;
+}
+// Resolves an offset code against the block's incoming repeat offsets.
+// Returns 0 and *off, or the reference's error for this decode_offset.
+constexpr uint64_t OFF_HUGE = ~0ull >> 1;
+ZD_HD inline int off_resolve(uint32_t v, const uint64_t in[3], uint64_t* off) {
+  if (v < OFF_SYM) { *off = v; return 0; }
+  if (v < OFF_GIANT) {
+    uint32_t slot = (v - OFF_SYM) >> 24, d = (v - OFF_SYM) & 0xFFFFFF;
+    uint64_t b = slot == 0 ? in[0] : (slot == 1 ? in[1] : in[2]);
+    if (b < d) return -90;                  // ZD_E_REF_PANIC (usize underflow)
+    *off = b - d;
+    return 0;
+  }
+  if (v == OFF_GIANT) { *off = OFF_HUGE; return 0; }
+  return v == OFF_NULL ? -41 /* ZD_E_NULL_OFFSET */ : -90 /* ZD_E_REF_PANIC */;
+}
 
 // ---------------------------------------------------------------------------
 // Error keys.  The reference parses every block of a frame (tables included)
@@ -88,6 +203,8 @@ struct CompState {
   uint32_t stop;           // nonzero: literals/sequences stage failed or is out of domain
   uint8_t al[3];           // accuracy log of the LL/OF/ML table in this block's FSE slot
   uint8_t huf_bits;        // maxBits of this block's LUT
+  uint32_t rep_out[3];     // repeat-offset codes after the block (symbolic in the incoming ones)
+  uint32_t _pad;
 };
 
 // Blocks of frames in order (all types).
@@ -119,7 +236,7 @@ struct FrameState {
 struct Workspace {
   uint64_t comp, comp_state, blocks, frames, frame_state;
   uint64_t list_tables, list_huf, list_seq;   // u32 work lists
-  uint64_t lits, seq_ll, seq_of, seq_ml, luts, fses;
+  uint64_t lits, seqs, luts, fses;
   uint64_t total;
 };
 

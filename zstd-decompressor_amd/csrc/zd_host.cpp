@@ -354,6 +354,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     int32_t huf_prev = prev_huf;
     int32_t tab_prev[3] = {prev_tab[0], prev_tab[1], prev_tab[2]};
     uint64_t bound = 0;
+    bool seqs_in_frame = false;
     bool frame_failed_host = hf.key != KEY_NONE;
     for (size_t bi = 0; bi < hf.blocks.size(); bi++) {
       HostBlock& hb = hf.blocks[bi];
@@ -406,6 +407,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
         }
         cb.seq_out = nseq_total;
         nseq_total += cb.nseq;
+        seqs_in_frame |= cb.nseq > 0;
         P->comps.push_back(cb);
         br.comp = (int32_t)ci;
         bool needs_tables = (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) ||
@@ -437,6 +439,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     }
     if (frame_failed_host) fd.nblocks = 0;
     if (fixed_cap) cap = fixed_cap;
+    // offset codes stay exact below 2^28 (zd_common.h); larger frames with
+    // sequences are outside the GPU path's domain
+    if (cap > MAX_FRAME_OUT && seqs_in_frame)
+      fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
     fd.out = out_off;
     fd.out_cap = cap;
     P->frame_cap_off.push_back(out_off);
@@ -457,11 +463,9 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
   W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
   W.lits = carve(lits + 64);
-  W.seq_ll = carve(4 * nseq_total + 64);
-  W.seq_of = carve(4 * nseq_total + 64);
-  W.seq_ml = carve(4 * nseq_total + 64);
+  W.seqs = carve(8 * nseq_total + 64);
   W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
-  W.fses = carve((uint64_t)FSE_ENTRIES * 4 * 3 * std::max<uint32_t>(fse_slots, 1));
+  W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint32_t>(fse_slots, 1));
   W.total = o;
 
   zd_plan_info& I = P->info;
@@ -724,7 +728,7 @@ int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t
   uint8_t *d_src = nullptr, *d_dst = nullptr;
   uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
   auto cleanup = [&]() { if (d_src) (void)hipFree(d_src); if (d_dst) (void)hipFree(d_dst); zd_plan_destroy(P); };
-  if (hipMalloc(&d_src, std::max<size_t>(n, 16)) != hipSuccess || hipMalloc(&d_dst, ob) != hipSuccess) {
+  if (hipMalloc(&d_src, n + ZD_SRC_PADDING) != hipSuccess || hipMalloc(&d_dst, ob) != hipSuccess) {
     cleanup(); return ZD_E_HIP;
   }
   if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) { cleanup(); return ZD_E_HIP; }
@@ -755,7 +759,7 @@ struct zd_context {
   uint64_t rep[3] = {1, 4, 8};
   // persisted tables of the previous blocks (one virtual comp block)
   uint16_t* d_lut = nullptr;    // LUT_ENTRIES
-  uint32_t* d_fse = nullptr;    // 3 * FSE_ENTRIES
+  uint16_t* d_fse = nullptr;    // FSE_SLOT entries
   uint8_t huf_bits = 0;
   uint8_t al[3] = {0, 0, 0};
   bool has_huf = false;
@@ -786,7 +790,7 @@ int zd_context_new(uint64_t window_size, zd_context** out) {
   zd_context* c = new (std::nothrow) zd_context();
   if (!c) return ZD_E_NO_MEMORY;
   c->window = window_size;
-  if (hipMalloc(&c->d_lut, LUT_ENTRIES * 2) != hipSuccess || hipMalloc(&c->d_fse, 3 * FSE_ENTRIES * 4) != hipSuccess) {
+  if (hipMalloc(&c->d_lut, LUT_ENTRIES * 2) != hipSuccess || hipMalloc(&c->d_fse, FSE_SLOT * 2) != hipSuccess) {
     zd_context_free(c);
     return ZD_E_HIP;
   }
@@ -820,7 +824,7 @@ int zd_context_offsets(const zd_context* c, uint64_t offsets[3]) {
 static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   uint8_t* d_src = nullptr;
   auto fin = [&](int r) { if (d_src) (void)hipFree(d_src); return r; };
-  if (hipMalloc(&d_src, std::max<size_t>(n, 16)) != hipSuccess) return ZD_E_HIP;
+  if (hipMalloc(&d_src, n + ZD_SRC_PADDING) != hipSuccess) return ZD_E_HIP;
   if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
   if (int r = upload_plan(P)) return fin(r);
   HIPCHK(hipMemset(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState)));
@@ -828,9 +832,9 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   if (P->has_prebuilt) {
     const CompBlock& pb = P->comps[0];
     uint8_t* luts = P->d_ws + P->W.luts + (uint64_t)pb.lut_slot * LUT_ENTRIES * 2;
-    uint8_t* fses = P->d_ws + P->W.fses + (uint64_t)pb.fse_slot * FSE_ENTRIES * 4 * 3;
+    uint8_t* fses = P->d_ws + P->W.fses + (uint64_t)pb.fse_slot * FSE_SLOT * 2;
     if (hipMemcpy(luts, c->d_lut, LUT_ENTRIES * 2, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
-    if (hipMemcpy(fses, c->d_fse, 3 * FSE_ENTRIES * 4, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
+    if (hipMemcpy(fses, c->d_fse, FSE_SLOT * 2, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
     CompState cs{};
     cs.huf_bits = c->huf_bits;
     for (int k = 0; k < 3; k++) cs.al[k] = c->al[k];
@@ -877,8 +881,8 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
       if (hipMemcpy(&ss, P->d_ws + P->W.comp_state + (size_t)srcc * sizeof(CompState), sizeof ss, hipMemcpyDeviceToHost) != hipSuccess)
         return fin(ZD_E_HIP);
       if ((size_t)srcc == ci) {
-        if (hipMemcpy(c->d_fse + k * FSE_ENTRIES,
-                      P->d_ws + P->W.fses + ((uint64_t)sb.fse_slot * 3 + k) * FSE_ENTRIES * 4, FSE_ENTRIES * 4,
+        if (hipMemcpy(c->d_fse + k * FSE_TAB,
+                      P->d_ws + P->W.fses + ((uint64_t)sb.fse_slot * FSE_SLOT + k * FSE_TAB) * 2, FSE_TAB * 2,
                       hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
         c->al[k] = ss.al[k];
       }
@@ -1028,16 +1032,21 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
     return rr;
   };
   if (r) return fin(r);
-  if (hipMalloc(&d_src, std::max<size_t>(nlits, 16)) != hipSuccess) return fin(ZD_E_HIP);
+  if (hipMalloc(&d_src, nlits + ZD_SRC_PADDING) != hipSuccess) return fin(ZD_E_HIP);
   if (nlits && hipMemcpy(d_src, lits, nlits, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
-  if (nseq) {
-    if (hipMemcpy(P.d_ws + P.W.seq_ll, ll, nseq * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(P.d_ws + P.W.seq_of, ofv, nseq * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(P.d_ws + P.W.seq_ml, ml, nseq * 4, hipMemcpyHostToDevice) != hipSuccess)
-      return fin(ZD_E_HIP);
-  }
+  // the caller's triples in K3's record format (offset codes symbolic in
+  // the context's repeat offsets; zd_common.h)
   CompState cs{};
   cs.lit_count = (uint32_t)nlits;
+  rep_init(cs.rep_out);
+  if (nseq) {
+    std::vector<uint64_t> rec(nseq);
+    for (size_t i = 0; i < nseq; i++) {
+      if (ll[i] > 0x1FFFF || ml[i] > 0x3FFFF) return fin(ZD_E_OUT_OF_DOMAIN);
+      rec[i] = seq_pack(ll[i], ml[i], rep_step(cs.rep_out, ofv[i], ll[i]));
+    }
+    if (hipMemcpy(P.d_ws + P.W.seqs, rec.data(), nseq * 8, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+  }
   if (hipMemcpy(P.d_ws + P.W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
   P.fdesc[0].out = 0;
   if (hipMemcpy(P.d_ws + P.W.frames, P.fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice) != hipSuccess)

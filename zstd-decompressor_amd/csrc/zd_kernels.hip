@@ -183,11 +183,11 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
 }
 
 // FseTable::from_distribution (fse.rs:110-202), serial.  State u of symbol s
-// (in position order) gets nextState = count(s) + u, nbits = al -
-// highbit(nextState), baseline = (nextState << nbits) - T, which equals the
-// reference's parts/base_width construction (fse.rs:169-189).  `-1` symbols
-// count as 1.  sym/next are LDS scratch (T and 256 entries).
-__device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint32_t* table, uint16_t* sym, uint16_t* next) {
+// (in position order) gets nextState = count(s) + u, stored with the symbol as
+// a 16-bit entry (zd_common.h fse_entry); nbits/baseline follow from it and
+// equal the reference's parts/base_width construction (fse.rs:169-189).
+// `-1` symbols count as 1.  sym/next are LDS scratch (T and 256 entries).
+__device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* table, uint16_t* sym, uint16_t* next) {
   if (al > FSE_MAX_AL) return ZD_E_LARGE_ACCURACY_LOG;
   uint32_t T = 1u << al;
   uint32_t zero_pos = T;
@@ -211,10 +211,7 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint32_t* t
   for (uint32_t s = 0; s < nsym; s++) next[s] = dist[s] > 0 ? (uint16_t)dist[s] : (dist[s] == -1 ? 1 : 0);
   for (uint32_t i = 0; i < T; i++) {
     uint32_t s = sym[i];
-    uint32_t ns = next[s]++;
-    int nb = al - highbit32(ns);
-    uint32_t base = (ns << nb) - T;
-    table[i] = fse_entry(s, (uint32_t)nb, base);
+    table[i] = fse_entry(s, next[s]++);
   }
   return 0;
 }
@@ -225,8 +222,8 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint32_t* t
 struct K1Smem {
   uint16_t lut[LUT_ENTRIES];        // 8 KiB
   uint16_t prefix[LUT_ENTRIES + 1]; // rare path: filled-entry prefix counts
-  uint32_t fse[FSE_ENTRIES];        // 2 KiB
-  uint16_t sym[FSE_ENTRIES];
+  uint16_t fse[FSE_TAB];            // 1 KiB
+  uint16_t sym[FSE_TAB];
   uint16_t next[256];
   int16_t dist[256];
   uint8_t weights[MAX_WEIGHTS];
@@ -264,12 +261,12 @@ __device__ void k1_huffman(const uint8_t* src, const uint8_t* src_end, const Com
         bool has_a = true, has_b = true;
         while (!st) {
           uint32_t cur = last_updated_is_first ? sb : sa;
-          uint32_t nb = (sm.fse[cur] >> 8) & 0xFF;
+          uint32_t nb = fse_nb(sm.fse[cur], al);
           if ((int64_t)nb > bs.bitpos) break;
           // symbol()
           uint32_t w;
-          if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = sm.fse[sb] & 0xFF; has_b = false; }
-          else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = sm.fse[sa] & 0xFF; has_a = false; }
+          if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sb]); has_b = false; }
+          else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sa]); has_a = false; }
           if (nw >= MAX_WEIGHTS - 2) { st = ZD_E_OUT_OF_DOMAIN; break; }
           sm.weights[nw++] = (uint8_t)w;
           // update_bits()
@@ -278,14 +275,14 @@ __device__ void k1_huffman(const uint8_t* src, const uint8_t* src_end, const Com
           if (has) { st = ZD_E_REF_PANIC; break; }
           st = bs.take((int)nb, &v);
           if (st) break;
-          s = (sm.fse[s] >> 16) + v;
+          s = fse_base(sm.fse[s], al) + v;
           has = true;
           last_updated_is_first = !last_updated_is_first;
         }
         for (int k = 0; k < 2 && !st; k++) {
           uint32_t w;
-          if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = sm.fse[sb] & 0xFF; has_b = false; }
-          else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = sm.fse[sa] & 0xFF; has_a = false; }
+          if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sb]); has_b = false; }
+          else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sa]); has_a = false; }
           sm.weights[nw++] = (uint8_t)w;
         }
       }
@@ -393,10 +390,10 @@ __device__ void k1_huffman(const uint8_t* src, const uint8_t* src_end, const Com
 
 // Sequence tables (sequences.rs:91-187): RLE bytes, FSE descriptions, predefined.
 __device__ void k1_sequences(const uint8_t* src, const CompBlock& C, uint32_t ci, CompState* cstate,
-                             FrameState* fstate, uint32_t* fses, K1Smem& sm) {
+                             FrameState* fstate, uint16_t* fses, K1Smem& sm) {
   const int lane = threadIdx.x;
   const uint8_t* blk = src + C.src;
-  uint32_t* slot = fses + (uint64_t)C.fse_slot * 3 * FSE_ENTRIES;
+  uint16_t* slot = fses + (uint64_t)C.fse_slot * FSE_SLOT;
   uint32_t pos = C.seq_tables;
   for (int k = 0; k < 3; k++) {
     int mode = C.modes[k];
@@ -404,7 +401,7 @@ __device__ void k1_sequences(const uint8_t* src, const CompBlock& C, uint32_t ci
       int st = 0, al = 0;
       if (mode == M_RLE) {
         if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
-        else { sm.fse[0] = fse_entry(blk[pos], 0, 0); pos++; }
+        else { sm.fse[0] = fse_entry(blk[pos], 1); pos++; }   // AL 0: nb 0, baseline 0
       } else if (mode == M_FSE) {
         if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
         else {
@@ -433,7 +430,7 @@ __device__ void k1_sequences(const uint8_t* src, const CompBlock& C, uint32_t ci
     }
     if (mode != M_REPEAT) {
       uint32_t T = 1u << sm.p;
-      for (uint32_t e = lane; e < T; e += 64) slot[k * FSE_ENTRIES + e] = sm.fse[e];
+      for (uint32_t e = lane; e < T; e += 64) slot[k * FSE_TAB + e] = sm.fse[e];
       if (lane == 0) cstate[ci].al[k] = (uint8_t)sm.p;
     }
     __syncthreads();
@@ -449,7 +446,7 @@ __device__ void k1_sequences(const uint8_t* src, const CompBlock& C, uint32_t ci
 __global__ __launch_bounds__(64) void zd_k_tables(const uint8_t* __restrict__ src, uint64_t src_size,
                                                   const CompBlock* __restrict__ comp, CompState* cstate,
                                                   FrameState* fstate, const uint32_t* __restrict__ list,
-                                                  uint16_t* luts, uint32_t* fses) {
+                                                  uint16_t* luts, uint16_t* fses) {
   __shared__ K1Smem sm;
   const uint32_t ci = list[blockIdx.x];
   const CompBlock C = comp[ci];
@@ -461,71 +458,182 @@ __global__ __launch_bounds__(64) void zd_k_tables(const uint8_t* __restrict__ sr
 }
 
 // ---------------------------------------------------------------------------
-// K2: Huffman literals.  Stream k decodes to k * ceil(R/4) (RFC 8878 §3.1.1.3.1.6);
-// the reference concatenates streams decoded until empty (literals.rs:68-81),
-// which is the same bytes whenever each stream holds its RFC share.
+// Per-lane backward bitstream windows (K2, K3)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void zd_k_huffman(const uint8_t* __restrict__ src, uint64_t src_size,
-                                                   const CompBlock* __restrict__ comp, CompState* cstate,
-                                                   FrameState* fstate, const uint32_t* __restrict__ list,
-                                                   const uint16_t* __restrict__ luts, uint8_t* lits) {
-  __shared__ uint16_t lut[LUT_ENTRIES];
-  __shared__ uint32_t counts[4];
-  __shared__ int errs[4];
-  const int lane = threadIdx.x;
-  const uint32_t ci = list[blockIdx.x];
-  const CompBlock C = comp[ci];
-  const uint64_t key0 = fstate[C.frame].key;
-  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
-  const uint32_t hs = (uint32_t)C.huf_src;
-  const int p = cstate[hs].huf_bits;
-  if (p == 0) {   // LUT not built (K1 stopped: parse error or out of domain)
-    if (lane == 0) cstate[ci].stop = 1;
-    return;
-  }
-  const uint32_t T = 1u << p;
-  const uint16_t* g = luts + (uint64_t)comp[hs].lut_slot * LUT_ENTRIES;
-  for (uint32_t e = lane; e < T; e += 64) lut[e] = g[e];
-  __syncthreads();
-  const int m = C.nstreams;
-  const uint32_t R = C.lit_regen;
-  const uint32_t seg = (R + 3) / 4;
-  if (lane < m) {
-    const uint32_t* ssz = comp[ci].stream_size;
-    uint32_t off = C.streams;
-    for (int j = 0; j < lane; j++) off += ssz[j];
-    const uint32_t start = (uint32_t)lane * seg;
-    const uint32_t cap = lane < m - 1 ? seg : (R > start ? R - start : 0);
-    uint8_t* out = lits + C.lit_out + start;
-    BwBits bs;
-    int st = bs.init(src + C.src + off, ssz[lane], src, src + src_size);
-    uint32_t count = 0;
-    while (!st && bs.bitpos > 0) {
-      uint32_t idx = bs.peek(p);
-      uint32_t e = lut[idx];
-      uint32_t nb = (e >> 8) & 0x7F;
-      if (e & LUT_ABSENT) {
-        st = ((int64_t)nb <= bs.bitpos) ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
-        break;
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef __attribute__((address_space(1))) const u32x4a4 g_u32x4a4;   // global (HBM) window loads
+typedef __attribute__((address_space(3))) uint16_t lds_u16;          // LDS tables
+typedef __attribute__((address_space(1))) const uint16_t g_u16;      // HBM tables
+
+// 16 bytes at a 4-aligned address ending at or after the byte holding bit
+// pos-1 of the stream at s; `bit` = stream bit index of w0's bit 0.  The
+// window covers at least 97 bits below pos (>= the 90 bits one sequence can
+// consume: 63 extra + 27 state bits).
+struct Win {
+  uint64_t w0, w1;
+  int32_t bit;
+};
+__device__ inline Win win_load(const uint8_t* s, uintptr_t lo, int32_t pos) {
+  // branch-free: a = max(lo, align_up(top - 16, 4)); pos may be slightly
+  // negative after a failing step, which also clamps to lo
+  const intptr_t top = (intptr_t)s + ((pos + 7) >> 3);
+  uintptr_t a = (uintptr_t)(top - 13) & ~(uintptr_t)3;
+  a = a < lo ? lo : a;
+  u32x4a4 v = *(g_u32x4a4*)a;
+  Win w;
+  w.w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  w.w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  w.bit = (int32_t)((intptr_t)a - (intptr_t)s) * 8;
+  return w;
+}
+// bits [r-64, r) of the 128-bit window, r = pos - bit in [0, 128]; branch-free
+// (64-bit shifts on gfx950 take the amount mod 64, so the edges are selects)
+__device__ inline uint64_t win_top(const Win& w, int32_t pos) {
+  const int r = pos - w.bit;
+  const int sh = r - 64;                             // >= 0: funnel of w1:w0
+  const uint64_t f_lo = sh >= 64 ? 0 : (w.w0 >> (sh & 63));
+  const uint64_t f_hi = sh <= 0 ? 0 : (w.w1 << ((64 - sh) & 63));
+  const uint64_t low = r <= 0 ? 0 : (w.w0 << ((64 - r) & 63));
+  return sh >= 0 ? (f_lo | f_hi) : low;
+}
+// MSB-first field of k bits from the top of t, k in [0, 63], no selects:
+// (t >> 1) >> (63 - k) is 0 for k = 0.
+__device__ inline uint32_t take_top(uint64_t& t, uint32_t k) {
+  const uint32_t v = (uint32_t)((t >> 1) >> (63 - k));
+  t <<= k;
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// K2: Huffman literals (literals.rs:49-86 + huffman.rs:205-218), one STREAM
+// per lane: a workgroup (one wave) takes K2_BLOCKS blocks, 4 lanes each, the
+// blocks' LUTs in LDS.  Each lane walks its stream through a 16-byte register
+// window, K2_GROUP symbols per window (<= 88 bits of a >= 97-bit window), and
+// stores the group's bytes with one 8-byte store.  Stream k decodes to
+// k * ceil(R/4) (RFC 8878 3.1.1.3.1.6); the reference concatenates streams
+// decoded until empty (literals.rs:68-81), which is the same bytes whenever
+// each stream holds its RFC share.  A block whose tree is deeper than 11 bits
+// makes its workgroup read LUTs from HBM.
+// ---------------------------------------------------------------------------
+constexpr int K2_BLOCKS = 8;
+constexpr int K2_LANES = 4 * K2_BLOCKS;
+constexpr int K2_LUT_BITS = 11;
+constexpr int K2_GROUP = 8;
+static_assert(K2_LANES <= 64, "K2 workgroup must be a single wave");
+static_assert(K2_GROUP * LUT_MAX_BITS <= 97, "a group must fit one window");
+typedef __attribute__((address_space(1))) uint64_t g_u64a1 __attribute__((aligned(1)));
+
+template <typename LP>
+__device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t lo, LP lut, int p, uint8_t* out,
+                          uint32_t cap, uint32_t* count_out) {
+  uint32_t count = 0;
+  *count_out = 0;
+  if (size == 0) return ZD_E_EMPTY_INPUT_DATA;
+  const uint8_t lastb = bs[size - 1];
+  if (lastb == 0) return ZD_E_NULL_BYTE;
+  int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
+  int st = 0;
+  while (pos > 0 && !st) {
+    const Win w = win_load(bs, lo, pos);
+    uint64_t acc = 0;
+    int got = 0;
+#pragma unroll
+    for (int j = 0; j < K2_GROUP; j++) {
+      if (pos > 0 && !st) {
+        uint32_t idx = (uint32_t)(win_top(w, pos) >> (64 - p));
+        if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
+        const uint32_t e = lut[idx];
+        const int32_t nb = (int32_t)((e >> 8) & 0x7F);
+        if (e & LUT_ABSENT) st = nb <= pos ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
+        else if (nb > pos) st = ZD_E_NOT_ENOUGH_BITS;
+        else {
+          pos -= nb;
+          acc |= (uint64_t)(e & 0xFF) << (8 * got);
+          got++;
+        }
       }
-      if ((int64_t)nb > bs.bitpos) { st = ZD_E_NOT_ENOUGH_BITS; break; }
-      bs.bitpos -= nb;
-      if (count < cap) out[count] = (uint8_t)e;
-      count++;
     }
-    counts[lane] = count;
-    errs[lane] = st;
-    if (st) key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, lane, st));
+    if (count + K2_GROUP <= cap && got == K2_GROUP) {
+      *(g_u64a1*)(out + count) = acc;
+    } else {
+      for (int j = 0; j < got; j++)
+        if (count + j < cap) out[count + j] = (uint8_t)(acc >> (8 * j));
+    }
+    count += got;
+  }
+  *count_out = count;
+  return st;
+}
+
+__global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restrict__ src,
+                                                         const CompBlock* __restrict__ comp, CompState* cstate,
+                                                         FrameState* fstate, const uint32_t* __restrict__ list,
+                                                         uint32_t n_list, const uint16_t* __restrict__ luts,
+                                                         uint8_t* lits) {
+  __shared__ __attribute__((aligned(16))) uint16_t lut[K2_BLOCKS][1 << K2_LUT_BITS];
+  __shared__ uint32_t counts[K2_BLOCKS][4];
+  __shared__ int errs[K2_BLOCKS][4];
+  const int lane = threadIdx.x, b = lane >> 2, k = lane & 3;
+  const uint32_t li = blockIdx.x * K2_BLOCKS + b;
+  bool act = li < n_list;
+  const uint32_t ci = act ? list[li] : 0;
+  CompBlock C;
+  if (act) C = comp[ci];
+  if (act) {
+    const uint64_t key0 = fstate[C.frame].key;
+    if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) act = false;
+  }
+  int p = 0;
+  const uint16_t* g = nullptr;
+  if (act) {
+    const uint32_t hs = (uint32_t)C.huf_src;
+    p = cstate[hs].huf_bits;
+    g = luts + (uint64_t)comp[hs].lut_slot * LUT_ENTRIES;
+    if (p == 0) {            // LUT not built (K1 stopped: parse error or out of domain)
+      if (k == 0) cstate[ci].stop = 1;
+      act = false;
+    }
+  }
+  const bool use_lds = __ballot(act && p > K2_LUT_BITS) == 0;
+  if (use_lds && act) {      // the block's 4 lanes copy its LUT, 16 bytes at a time
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const u32x4 g_u4;
+    typedef __attribute__((address_space(3))) u32x4 l_u4;
+    const int n16 = (1 << p) / 8;
+    if (n16 == 0) { if (k == 0) for (int e = 0; e < (1 << p); e++) lut[b][e] = g[e]; }
+    else for (int e = k; e < n16; e += 4) ((l_u4*)lut[b])[e] = ((g_u4*)g)[e];
   }
   __syncthreads();
-  if (lane == 0) {
+  const int m = act ? C.nstreams : 0;
+  const uint32_t R = act ? C.lit_regen : 0;
+  const uint32_t seg = (R + 3) / 4;
+  if (act && k < m) {
+    uint32_t off = C.streams;
+    for (int j = 0; j < k; j++) off += C.stream_size[j];
+    const uint32_t start = (uint32_t)k * seg;
+    const uint32_t cap = k < m - 1 ? seg : (R > start ? R - start : 0);
+    const uint8_t* blk = src + C.src;
+    const uintptr_t lo = (uintptr_t)blk & ~(uintptr_t)3;
+    uint32_t count;
+    int st;
+    if (use_lds)
+      st = huf_stream<const lds_u16*>(blk + off, C.stream_size[k], lo, (const lds_u16*)lut[b], p,
+                                      lits + C.lit_out + start, cap, &count);
+    else
+      st = huf_stream<g_u16*>(blk + off, C.stream_size[k], lo, (g_u16*)g, p, lits + C.lit_out + start, cap, &count);
+    counts[b][k] = count;
+    errs[b][k] = st;
+    if (st) key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, k, st));
+  }
+  __syncthreads();
+  if (act && k == 0) {
     bool err = false, ood = false;
-    for (int k = 0; k < m; k++) err |= errs[k] != 0;
+    for (int j = 0; j < m; j++) err |= errs[b][j] != 0;
     uint32_t total = 0;
-    for (int k = 0; k < m && !err; k++) {
-      uint32_t cap = k < m - 1 ? seg : (R > (uint32_t)k * seg ? R - (uint32_t)k * seg : 0);
-      if (k < m - 1 ? counts[k] != seg : counts[k] > cap) ood = true;
-      total += counts[k];
+    for (int j = 0; j < m && !err; j++) {
+      const uint32_t cap = j < m - 1 ? seg : (R > (uint32_t)j * seg ? R - (uint32_t)j * seg : 0);
+      if (j < m - 1 ? counts[b][j] != seg : counts[b][j] > cap) ood = true;
+      total += counts[b][j];
     }
     if (ood && !err) key_min(fstate, C.frame, make_key(PH_LIMIT, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
     cstate[ci].lit_count = total;
@@ -534,64 +642,153 @@ __global__ __launch_bounds__(64) void zd_k_huffman(const uint8_t* __restrict__ s
 }
 
 // ---------------------------------------------------------------------------
-// K3: sequences (sequences.rs:191-237, decoders/sequence.rs:41-88)
+// K3: sequences (sequences.rs:191-237, decoders/sequence.rs:30-93), one block
+// per LANE.  The FSE chain of a block is strictly serial, so parallelism comes
+// from blocks: each lane runs one block's three-state machine with its tables
+// in LDS (16-bit entries, LL 512 | ML 512 | OF 256 per lane), the bitstream
+// read through a 128-bit register window that is reloaded one step ahead
+// (the next step's exact bit position is known once this step's table
+// entries are read, so the reload's latency hides behind the rest of the
+// step).  Offsets leave as repeat-offset codes (zd_common.h), symbolic in the
+// block's incoming repeat offsets, so blocks of one frame decode in parallel.
+// A lane whose OF table is deeper than 256 states (AL 9; never produced by
+// zstd, whose offset tables are AL <= 8) makes its workgroup read tables from
+// HBM instead.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void zd_k_sequences(const uint8_t* __restrict__ src, uint64_t src_size,
-                                                     const CompBlock* __restrict__ comp, CompState* cstate,
-                                                     FrameState* fstate, const uint32_t* __restrict__ list,
-                                                     const uint32_t* __restrict__ fses, uint32_t* seq_ll,
-                                                     uint32_t* seq_of, uint32_t* seq_ml) {
-  __shared__ uint32_t tab[3][FSE_ENTRIES];
-  __shared__ int als[3];
+constexpr int K3_LANES = 32;
+constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
+constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
+static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
+
+// Runs one block's sequences; TP is an LDS (lds_u16*) or HBM (g_u16*) table
+// pointer.  Returns 0 or the reference's error.
+template <typename TP>
+__device__ int seq_block(const uint8_t* bs, uint32_t bs_size, uintptr_t lo, TP tll, TP tml, TP tof, int all,
+                         int alo, int alm, uint32_t n, uint64_t* __restrict__ out, uint32_t rep[3]) {
+  // BackwardBitParser::new (parsing.rs:200-220)
+  if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return ZD_E_NULL_BYTE;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
+  Win w = win_load(bs, lo, pos);
+  // SequenceDecoder::initialize: LL, OF, ML (sequence.rs:59-65)
+  if (all + alo + alm > pos) return ZD_E_NOT_ENOUGH_BITS;
+  uint64_t t0 = win_top(w, pos);
+  uint32_t sLL = take_top(t0, all), sOF = take_top(t0, alo), sML = take_top(t0, alm);
+  pos -= all + alo + alm;
+  w = win_load(bs, lo, pos);
+  // consume the first window here, so the loop head's wait covers only the
+  // latch's load (vmcnt(1): the step's store may stay in flight)
+  asm volatile("" : "+v"(w.w0), "+v"(w.w1));
+  // nb = AL - highbit(ns) = clz(ns) + (AL - 31)
+  const int aL = all - 31, aM = alm - 31, aO = alo - 31;
+  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
+  // One exit at the bottom and no other branches: the body is straight-line,
+  // so the next window's load lands directly in the window registers (no
+  // copy that would wait on it).  A failing step still runs to the bottom:
+  // states stay inside their tables (valid FSE tables map every state and
+  // bit pattern to a state < T) and window loads clamp, so nothing strays.
+  int st = 0;
+  for (uint32_t i = 0;; i++) {
+    const uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
+    const uint32_t llc = eLL & 63, ofc = eOF & 63, mlc = eML & 63;
+    const bool codemax = llc > 35 || mlc > 52 || ofc > 31;
+    uint32_t llbase, llb, mlbase, mlb;
+    ll_code(llc, &llbase, &llb);
+    ml_code(mlc, &mlbase, &mlb);
+    const uint32_t nsL = eLL >> 6, nsM = eML >> 6, nsO = eOF >> 6;
+    const uint32_t nbL = __clz(nsL) + aL, nbM = __clz(nsM) + aM, nbO = __clz(nsO) + aO;
+    const int32_t E = (int32_t)((ofc & 31) + mlb + llb);
+    const bool last = i + 1 == n;
+    const int32_t S = last ? 0 : (int32_t)(nbL + nbM + nbO);
+    st = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : (E + S > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
+    // every use of this step's window precedes the next window's load, and
+    // the load precedes this step's store: the next step waits on the load only
+    uint64_t t = win_top(w, pos);
+    uint64_t t2 = win_top(w, pos - E);
+    pos -= E + S;
+    asm volatile("" : "+v"(t), "+v"(t2)::"memory");   // the window's reads stay above its reload
+    w = win_load(bs, lo, pos);
+    // update_symbol_value (sequence.rs:41-55): OF, ML, LL extra bits
+    const uint32_t ob = take_top(t, ofc & 31), mb = take_top(t, mlb), lb = take_top(t, llb);
+    const uint32_t ofv = (1u << (ofc & 31)) + ob, ml = mlbase + mb, ll = llbase + lb;
+    out[i] = seq_pack(ll, ml, rep_step(rep, ofv, ll));
+    // update_bits: LL, ML, OF (sequence.rs:80-88)
+    const uint32_t vL = take_top(t2, nbL), vM = take_top(t2, nbM), vO = take_top(t2, nbO);
+    sLL = ((nsL << nbL) - TL) + vL;
+    sML = ((nsM << nbM) - TM) + vM;
+    sOF = ((nsO << nbO) - TO) + vO;
+    if (st != 0 || last) break;
+  }
+  return st;
+}
+
+__global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __restrict__ src,
+                                                           const CompBlock* __restrict__ comp, CompState* cstate,
+                                                           FrameState* fstate, const uint32_t* __restrict__ list,
+                                                           uint32_t n_list, const uint16_t* __restrict__ fses,
+                                                           uint64_t* __restrict__ seqs) {
+  __shared__ __attribute__((aligned(16))) uint16_t tabs[K3_LANES * K3_TAB];
   const int lane = threadIdx.x;
-  const uint32_t ci = list[blockIdx.x];
-  const CompBlock C = comp[ci];
-  const uint64_t key0 = fstate[C.frame].key;
-  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
-  for (int k = 0; k < 3; k++) {
-    const uint32_t s = (uint32_t)C.tab_src[k];
-    const int al = cstate[s].al[k];
-    const uint32_t* g = fses + ((uint64_t)comp[s].fse_slot * 3 + k) * FSE_ENTRIES;
-    for (uint32_t e = lane; e < (1u << al); e += 64) tab[k][e] = g[e];
-    if (lane == 0) als[k] = al;
+  const uint32_t li = blockIdx.x * K3_LANES + lane;
+  bool act = li < n_list;
+  const uint32_t ci = act ? list[li] : 0;
+  CompBlock C;
+  if (act) C = comp[ci];
+  if (act) {
+    const uint64_t key0 = fstate[C.frame].key;
+    if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) act = false;
+  }
+  int al[3] = {0, 0, 0};
+  const uint16_t* g[3] = {nullptr, nullptr, nullptr};
+  if (act) {
+    for (int k = 0; k < 3; k++) {
+      const uint32_t s = (uint32_t)C.tab_src[k];
+      al[k] = cstate[s].al[k];
+      g[k] = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+    }
+  }
+  // tables -> LDS (every lane its own three), unless some lane needs AL 9 offsets
+  const bool deep = act && al[1] > 8;
+  const bool use_lds = __ballot(deep) == 0;      // the workgroup is one wave
+  lds_u16* mine = (lds_u16*)tabs + lane * K3_TAB;
+  if (use_lds && act) {
+    const int cnt[3] = {1 << al[0], 1 << al[1], 1 << al[2]};
+    const int dst[3] = {0, K3_TL + K3_TM, K3_TL};     // LL | ML | OF in LDS
+    for (int k = 0; k < 3; k++) {
+      if (cnt[k] >= 8) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const u32x4 g_u4;
+        typedef __attribute__((address_space(3))) u32x4 l_u4;
+        g_u4* s4 = (g_u4*)g[k];
+        l_u4* d4 = (l_u4*)(mine + dst[k]);
+        for (int e = 0; e < cnt[k] / 8; e++) d4[e] = s4[e];
+      } else {
+        for (int e = 0; e < cnt[k]; e++) mine[dst[k] + e] = ((g_u16*)g[k])[e];
+      }
+    }
   }
   __syncthreads();
-  if (lane != 0) return;
+  if (!act) return;
   const CompState cs = cstate[ci];
-  BwBits bs;
-  int st = bs.init(src + C.src + cs.bs_off, cs.bs_size, src, src + src_size);
-  uint32_t sLL = 0, sOF = 0, sML = 0, v;
-  // SequenceDecoder::initialize: LL, OF, ML (sequence.rs:59-65)
-  if (!st) st = bs.take(als[0], &sLL);
-  if (!st) st = bs.take(als[1], &sOF);
-  if (!st) st = bs.take(als[2], &sML);
-  uint32_t* oll = seq_ll + C.seq_out;
-  uint32_t* oof = seq_of + C.seq_out;
-  uint32_t* oml = seq_ml + C.seq_out;
-  const uint32_t n = C.nseq;
-  for (uint32_t i = 0; i < n && !st; i++) {
-    const uint32_t eLL = tab[0][sLL], eOF = tab[1][sOF], eML = tab[2][sML];
-    const uint32_t llc = eLL & 0xFF, ofc = eOF & 0xFF, mlc = eML & 0xFF;
-    if (llc > 35 || mlc > 52 || ofc > 31) { st = ZD_E_SEQUENCE_CODE_MAX_EXCEEDED; break; }
-    uint32_t ob, mb, lb;
-    if ((st = bs.take((int)ofc, &ob))) break;
-    if ((st = bs.take(c_ml_bits[mlc], &mb))) break;
-    if ((st = bs.take(c_ll_bits[llc], &lb))) break;
-    oof[i] = (1u << ofc) + ob;
-    oml[i] = c_ml_base[mlc] + mb;
-    oll[i] = c_ll_base[llc] + lb;
-    if (i + 1 == n) break;
-    // update_bits: LL, ML, OF (sequence.rs:80-88)
-    if ((st = bs.take((eLL >> 8) & 0xFF, &v))) break;
-    sLL = (eLL >> 16) + v;
-    if ((st = bs.take((eML >> 8) & 0xFF, &v))) break;
-    sML = (eML >> 16) + v;
-    if ((st = bs.take((eOF >> 8) & 0xFF, &v))) break;
-    sOF = (eOF >> 16) + v;
-  }
+  const uint8_t* blk = src + C.src;
+  const uintptr_t lo = (uintptr_t)blk & ~(uintptr_t)3;
+  uint32_t rep[3];
+  rep_init(rep);
+  int st;
+  if (use_lds)
+    st = seq_block<const lds_u16*>(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM,
+                                   al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
+  else
+    st = seq_block<g_u16*>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2],
+                           (g_u16*)g[1], al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
   if (st) {
     key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
     cstate[ci].stop = 1;
+  } else {
+    cstate[ci].rep_out[0] = rep[0];
+    cstate[ci].rep_out[1] = rep[1];
+    cstate[ci].rep_out[2] = rep[2];
   }
 }
 
@@ -602,46 +799,6 @@ constexpr int RING = 8192;
 constexpr uint32_t RMASK = RING - 1;
 constexpr uint32_t BATCH = 2048;
 
-// Repeat-offset update as a transform of the 3-entry state: entry j of the
-// result is either state[src_j] + val_j (src_j in 0..2) or the constant val_j
-// (src_j == 3).  decoding_context.rs:50-75 per (offset_value, ll).
-struct RepT {
-  uint32_t src;      // 2 bits per entry
-  int64_t v[3];
-};
-
-__device__ inline RepT rep_of(uint32_t ofv, uint32_t ll) {
-  RepT t;
-  t.v[0] = t.v[1] = t.v[2] = 0;
-  auto S = [](uint32_t a, uint32_t b, uint32_t c) { return a | (b << 2) | (c << 4); };
-  if (ofv > 3) { t.src = S(3, 0, 1); t.v[0] = (int64_t)ofv - 3; }
-  else if (ofv == 3 && ll == 0) { t.src = S(0, 0, 1); t.v[0] = -1; }
-  else if (ofv == 3 || (ofv == 2 && ll == 0)) t.src = S(2, 0, 1);
-  else if (ofv == 2 || (ofv == 1 && ll == 0)) t.src = S(1, 0, 2);
-  else t.src = S(0, 1, 2);   // (1, ll > 0): unchanged
-  return t;
-}
-
-// (g after f)
-__device__ inline int64_t sel3(int64_t a, int64_t b, int64_t c, uint32_t s) { return s == 0 ? a : (s == 1 ? b : c); }
-
-__device__ inline RepT rep_compose(const RepT& g, const RepT& f) {
-  RepT r;
-  r.src = 0;
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-    uint32_t s = (g.src >> (2 * j)) & 3;
-    if (s == 3) { r.src |= 3u << (2 * j); r.v[j] = g.v[j]; }
-    else { r.src |= ((f.src >> (2 * s)) & 3) << (2 * j); r.v[j] = sel3(f.v[0], f.v[1], f.v[2], s) + g.v[j]; }
-  }
-  return r;
-}
-
-__device__ inline int64_t shfl_up_i64(int64_t x, int d) {
-  int lo = __shfl_up((int)(uint32_t)x, d, 64);
-  int hi = __shfl_up((int)(uint32_t)((uint64_t)x >> 32), d, 64);
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
 __device__ inline int64_t readlane_i64(int64_t x, int l) {
   int lo = __shfl((int)(uint32_t)x, l, 64);
   int hi = __shfl((int)(uint32_t)((uint64_t)x >> 32), l, 64);
@@ -707,9 +864,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
                                                    const CompBlock* __restrict__ comp,
                                                    const CompState* __restrict__ cstate,
                                                    const uint8_t* __restrict__ lits,
-                                                   const uint32_t* __restrict__ seq_ll,
-                                                   const uint32_t* __restrict__ seq_of,
-                                                   const uint32_t* __restrict__ seq_ml) {
+                                                   const uint64_t* __restrict__ seqs) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
   __shared__ uint8_t stage[BATCH];
   const int lane = threadIdx.x;
@@ -732,7 +887,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
     uint64_t lo = X.pos > (uint64_t)RING ? X.pos - RING : 0;
     for (uint64_t p = lo + lane; p < X.pos; p += 64) X.R(p) = X.out[p];
   }
-  int64_t rep[3] = {(int64_t)S->rep[0], (int64_t)S->rep[1], (int64_t)S->rep[2]};
+  uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
   uint64_t err_key = KEY_NONE;
 
   for (uint32_t j = 0; j < F.nblocks && err_key == KEY_NONE; j++) {
@@ -757,33 +912,17 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
     else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle; nl = C.lit_regen; }
     else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
     uint64_t lit_cursor = 0;
-    const uint32_t* LL = seq_ll + C.seq_out;
-    const uint32_t* OF = seq_of + C.seq_out;
-    const uint32_t* ML = seq_ml + C.seq_out;
+    const uint64_t* SQ = seqs + C.seq_out;
     const uint32_t n = C.nseq;
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
       const uint32_t i = s0 + lane;
       const bool valid = i < n;
-      const uint32_t ll = valid ? LL[i] : 0;
-      const uint32_t ofv = valid ? OF[i] : 1;
-      const uint32_t ml = valid ? ML[i] : 0;
-      // repeat offsets: inclusive scan of transforms, then apply to `rep`
-      RepT t = valid ? rep_of(ofv, ll) : rep_of(1, 1);
-      for (int d = 1; d < 64; d <<= 1) {
-        RepT u;
-        u.src = __shfl_up(t.src, d, 64);
-        u.v[0] = shfl_up_i64(t.v[0], d);
-        u.v[1] = shfl_up_i64(t.v[1], d);
-        u.v[2] = shfl_up_i64(t.v[2], d);
-        if (lane >= d) t = rep_compose(t, u);
-      }
-      int64_t after[3];
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        uint32_t s = (t.src >> (2 * k)) & 3;
-        after[k] = s == 3 ? t.v[k] : sel3(rep[0], rep[1], rep[2], s) + t.v[k];
-      }
-      const int64_t off = after[0];
+      const uint64_t sq = valid ? SQ[i] : 0;
+      const uint32_t ll = seq_ll(sq), ml = seq_ml(sq);
+      // decode_offset (decoding_context.rs:50-75): K3's code against the block's incoming offsets
+      uint64_t offu = 0;
+      const int derr = valid ? off_resolve(seq_off(sq), rep, &offu) : 0;
+      const int64_t off = (int64_t)offu;
       // positions
       const uint32_t tot = ll + ml;
       const uint32_t inc_tot = scan_incl_u32(tot, lane);
@@ -791,18 +930,19 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
       // checks (decoding_context.rs:86-90, D9)
       const uint64_t before = X.pos + opos;
-      const bool imp = valid && ((uint64_t)ll > nl - (lit_cursor + lpos) || lit_cursor + lpos > nl ||
-                                 (off > 0 && (uint64_t)off > before + ll));
-      const bool panic = valid && !imp && off <= 0;
-      const uint64_t badm = __ballot(imp || panic);
+      const bool dbad = valid && derr != 0;
+      const bool imp = valid && !dbad && ((uint64_t)ll > nl - (lit_cursor + lpos) || lit_cursor + lpos > nl ||
+                                          offu > before + ll);
+      const bool panic = valid && !dbad && !imp && ml != 0 && offu == 0;
+      const uint64_t badm = __ballot(dbad || imp || panic);
       // batch: sequences whose bytes fit in BATCH
       const uint64_t fitm = __ballot(valid && inc_tot <= BATCH);
       uint32_t k = (uint32_t)__popcll(fitm);
       if (badm) {
         const int b = __ffsll((long long)badm) - 1;
         if ((uint32_t)b < (k ? k : 1u)) {
-          const bool bimp = __shfl((int)imp, b, 64);
-          err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0 + b, bimp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC);
+          const int code = __shfl(dbad ? derr : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
+          err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0 + b, code);
           break;
         }
       }
@@ -841,10 +981,6 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
           __syncthreads();
         }
         // advance
-        const int last = (int)k - 1;
-        rep[0] = readlane_i64(after[0], last);
-        rep[1] = readlane_i64(after[1], last);
-        rep[2] = readlane_i64(after[2], last);
         lit_cursor += L;
         X.pos += T;
         s0 += k;
@@ -875,13 +1011,16 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
           k0 += P;
           X.flush();
         }
-        rep[0] = readlane_i64(after[0], 0);
-        rep[1] = readlane_i64(after[1], 0);
-        rep[2] = readlane_i64(after[2], 0);
         s0 += 1;
       }
     }
     if (err_key != KEY_NONE) break;
+    // repeat offsets after the block
+    if (n) {
+      uint64_t nr[3];
+      for (int k = 0; k < 3; k++) (void)off_resolve(CS.rep_out[k], rep, &nr[k]);
+      rep[0] = nr[0]; rep[1] = nr[1]; rep[2] = nr[2];
+    }
     // leftover literals (decoding_context.rs:101-103)
     if (lit_cursor < nl && !X.emit(lsrc ? lsrc + lit_cursor : nullptr, lfill, nl - lit_cursor))
       err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_DST_TOO_SMALL);
@@ -893,9 +1032,9 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
   X.final_flush();
   if (lane == 0) {
     S->out_len = X.pos;
-    S->rep[0] = (uint64_t)rep[0];
-    S->rep[1] = (uint64_t)rep[1];
-    S->rep[2] = (uint64_t)rep[2];
+    S->rep[0] = rep[0];
+    S->rep[1] = rep[1];
+    S->rep[2] = rep[2];
   }
 }
 
@@ -923,10 +1062,8 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   auto* frames = (const FrameDesc*)(ws + W.frames);
   auto* fstate = (FrameState*)(ws + W.frame_state);
   auto* luts = (uint16_t*)(ws + W.luts);
-  auto* fses = (uint32_t*)(ws + W.fses);
-  auto* sll = (uint32_t*)(ws + W.seq_ll);
-  auto* sof = (uint32_t*)(ws + W.seq_of);
-  auto* sml = (uint32_t*)(ws + W.seq_ml);
+  auto* fses = (uint16_t*)(ws + W.fses);
+  auto* seqs = (uint64_t*)(ws + W.seqs);
   hipStream_t s = a.stream;
   hipError_t e;
   if (a.events) if ((e = hipEventRecord(a.events[0], s)) != hipSuccess) return e;
@@ -935,17 +1072,16 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        (const uint32_t*)(ws + W.list_tables), luts, fses);
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
   if (a.n_huf)
-    hipLaunchKernelGGL(zd_k_huffman, dim3(a.n_huf), dim3(64), 0, s, a.src, a.src_size, comp, cstate, fstate,
-                       (const uint32_t*)(ws + W.list_huf), (const uint16_t*)luts, ws + W.lits);
+    hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s, a.src, comp,
+                       cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   if (a.n_seq)
-    hipLaunchKernelGGL(zd_k_sequences, dim3(a.n_seq), dim3(64), 0, s, a.src, a.src_size, comp, cstate, fstate,
-                       (const uint32_t*)(ws + W.list_seq), (const uint32_t*)fses, sll, sof, sml);
+    hipLaunchKernelGGL(zd_k_sequences, dim3((a.n_seq + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
+                       cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses, seqs);
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   if (a.n_frames)
     hipLaunchKernelGGL(zd_k_execute, dim3(a.n_frames), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
-                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint32_t*)sll,
-                       (const uint32_t*)sof, (const uint32_t*)sml);
+                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs);
   if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
   return hipGetLastError();
 }
