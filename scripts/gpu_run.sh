@@ -27,6 +27,8 @@ for s in "$@"; do
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline ;;
+    pmc) run pmc_sq 900 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify ;;
+    pmchbm) run pmc_fetch 900 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify && run pmc_write 900 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -187,21 +187,21 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
 // a 16-bit entry (zd_common.h fse_entry); nbits/baseline follow from it and
 // equal the reference's parts/base_width construction (fse.rs:169-189).
 // `-1` symbols count as 1.  sym/next are LDS scratch (T and 256 entries).
-__device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* table, uint16_t* sym, uint16_t* next) {
+__device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* table, uint8_t* sym, uint16_t* next) {
   if (al > FSE_MAX_AL) return ZD_E_LARGE_ACCURACY_LOG;
   uint32_t T = 1u << al;
   uint32_t zero_pos = T;
   for (uint32_t s = 0; s < nsym; s++) {
     if (dist[s] == -1) {
       if (zero_pos == 0) return ZD_E_REF_PANIC;
-      sym[--zero_pos] = (uint16_t)s;
+      sym[--zero_pos] = (uint8_t)s;
     }
   }
   uint32_t pos = 0, step = (T >> 1) + (T >> 3) + 3, mask = T - 1, placed = 0;
   for (uint32_t s = 0; s < nsym; s++) {
     for (int k = 0; k < dist[s]; k++) {
       if (zero_pos == 0) return ZD_E_REF_PANIC;   // the reference loops forever
-      sym[pos] = (uint16_t)s;
+      sym[pos] = (uint8_t)s;
       placed++;
       pos = (pos + step) & mask;
       while (pos >= zero_pos) pos = (pos + step) & mask;
@@ -217,244 +217,238 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* t
 }
 
 // ---------------------------------------------------------------------------
-// K1: tables
+// K1: tables, one compressed block per LANE (huffman.rs:80-203, fse.rs:16-202,
+// sequences.rs:91-187).  Every table build is serial code; running blocks on
+// lanes (instead of one block per wave with one lane busy) makes the whole
+// chip build tables at once.  Each lane keeps its scratch in LDS and writes
+// its Huffman LUT and compact FSE tables straight to the block's HBM slots.
 // ---------------------------------------------------------------------------
-struct K1Smem {
-  uint16_t lut[LUT_ENTRIES];        // 8 KiB
-  uint16_t prefix[LUT_ENTRIES + 1]; // rare path: filled-entry prefix counts
-  uint16_t fse[FSE_TAB];            // 1 KiB
-  uint16_t sym[FSE_TAB];
+constexpr int K1_LANES = 16;
+constexpr int K1_MAX_WEIGHTS = 255;               // a Huffman tree of 256 symbols (RFC 8878 4.2.1)
+struct K1Lane {
+  uint16_t fse[FSE_TAB];                          // Huffman-weight FSE table
+  uint8_t sym[FSE_TAB];                           // spread scratch
   uint16_t next[256];
   int16_t dist[256];
-  uint8_t weights[MAX_WEIGHTS];
-  uint8_t widths[MAX_WEIGHTS + 1];
-  int status;
-  int p;
-  uint32_t n;
-  int holes;
+  uint8_t weights[K1_MAX_WEIGHTS + 1];
+  uint16_t cnt[16], start[16], placed[16];        // per code width (<= 12)
 };
 
-// Huffman description -> LUT (huffman.rs:80-203).  Lane 0 parses; the wave fills.
-__device__ void k1_huffman(const uint8_t* src, const uint8_t* src_end, const CompBlock& C, uint32_t ci,
-                           CompState* cstate, FrameState* fstate, uint16_t* luts, K1Smem& sm) {
-  const int lane = threadIdx.x;
-  const uint8_t* desc = src + C.src + C.lit_data;
-  if (lane == 0) {
-    int st = 0;
-    uint32_t nw = 0;
-    uint8_t h = desc[0];
-    if (h < 128) {
-      // parse_fse (huffman.rs:108-130)
-      FwBits fw{desc + 1, h, 0};
-      uint8_t al;
-      uint32_t nsym;
-      st = parse_ncount(fw, &al, sm.dist, &nsym);
-      if (!st) st = build_fse(al, sm.dist, nsym, sm.fse, sm.sym, sm.next);
-      BwBits bs;
-      if (!st) st = bs.init(desc + 1 + fw.bytes_read(), h - fw.bytes_read(), src, src_end);
-      if (!st) {
-        // AlternatingDecoder (alternating.rs): initialize first, second
-        uint32_t sa = 0, sb = 0, v;
-        st = bs.take(al, &sa);
-        if (!st) st = bs.take(al, &sb);
-        bool last_updated_is_first = false, last_read_is_first = false;
-        bool has_a = true, has_b = true;
-        while (!st) {
-          uint32_t cur = last_updated_is_first ? sb : sa;
-          uint32_t nb = fse_nb(sm.fse[cur], al);
-          if ((int64_t)nb > bs.bitpos) break;
-          // symbol()
-          uint32_t w;
-          if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sb]); has_b = false; }
-          else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sa]); has_a = false; }
-          if (nw >= MAX_WEIGHTS - 2) { st = ZD_E_OUT_OF_DOMAIN; break; }
-          sm.weights[nw++] = (uint8_t)w;
-          // update_bits()
-          uint32_t& s = last_updated_is_first ? sb : sa;
-          bool& has = last_updated_is_first ? has_b : has_a;
-          if (has) { st = ZD_E_REF_PANIC; break; }
-          st = bs.take((int)nb, &v);
-          if (st) break;
-          s = fse_base(sm.fse[s], al) + v;
-          has = true;
-          last_updated_is_first = !last_updated_is_first;
-        }
-        for (int k = 0; k < 2 && !st; k++) {
-          uint32_t w;
-          if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sb]); has_b = false; }
-          else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(sm.fse[sa]); has_a = false; }
-          sm.weights[nw++] = (uint8_t)w;
-        }
-      }
-    } else {
-      // parse_direct (huffman.rs:92-106): high nibble first
-      nw = (uint32_t)h - 127;
-      for (uint32_t i = 0; i < nw; i++) {
-        uint8_t b = desc[1 + i / 2];
-        sm.weights[i] = (i & 1) ? (b & 15) : (b >> 4);
-      }
+// Entries [a, b) that no code reaches: the tree node there is Absent.  Its
+// depth is that of the largest aligned block around the entry inside [a, b)
+// (the entries just outside hold codes or lie past the table), which is the
+// number of bits HuffmanDecoder::decode (huffman.rs:205-218) reads before
+// it hits the node and panics.
+__device__ void lut_holes(uint16_t* lut, int p, uint32_t a, uint32_t b) {
+  for (uint32_t e = a; e < b; e++) {
+    int k = p;
+    for (; k > 0; k--) {
+      const uint32_t lo = e & ~((1u << k) - 1);
+      if (lo >= a && lo + (1u << k) <= b) break;
     }
-    // from_weights (huffman.rs:177-203)
-    int p = 0;
-    if (!st) {
-      uint32_t sum = 0;
-      for (uint32_t i = 0; i < nw && !st; i++) {
-        uint32_t w = sm.weights[i];
-        if (!w) continue;
-        if (w - 1 >= 32) { st = ZD_E_REF_PANIC; break; }
-        uint32_t add = 1u << (w - 1);
-        if (sum > 0xFFFFFFFFu - add) { st = ZD_E_REF_PANIC; break; }
-        sum += add;
-      }
-      if (!st && sum == 0) st = ZD_E_REF_PANIC;
-      if (!st) {
-        p = highbit32(sum);
-        if ((1ull << p) < sum) p++;
-        if (p >= 32) st = ZD_E_REF_PANIC;
-      }
-      uint32_t manquant = 0;
-      if (!st) {
-        uint8_t rest = (uint8_t)((1u << p) - sum);
-        if (rest == 0) st = ZD_E_REF_PANIC;   // D3
-        else manquant = (uint32_t)highbit32(rest) + 1;
-      }
-      for (uint32_t i = 0; i < nw && !st; i++) {
-        uint32_t w = sm.weights[i];
-        if (w && w > (uint32_t)p + 1) st = ZD_E_REF_PANIC;
-        sm.widths[i] = w ? (uint8_t)(p + 1 - w) : 0;
-      }
-      if (!st && manquant > (uint32_t)p + 1) st = ZD_E_REF_PANIC;
-      if (!st) sm.widths[nw] = (uint8_t)(p + 1 - manquant);
-      if (!st && p > LUT_MAX_BITS) st = ZD_E_OUT_OF_DOMAIN;
-    }
-    // from_number_of_bits + insert (huffman.rs:132-175): canonical placement,
-    // longest codes first, ascending symbol (u8), leftmost free aligned slot.
-    int holes = 0;
-    if (!st) {
-      uint32_t n = nw + 1, T = 1u << p, pos = 0;
-      for (uint32_t e = 0; e < T; e++) sm.lut[e] = 0xFFFF;
-      for (int w = p; w >= 1; w--) {
-        uint32_t S = 1u << (p - w);
-        for (uint32_t v = 0; v < 256; v++) {
-          for (uint32_t i = v; i < n; i += 256) {
-            if (sm.widths[i] != w) continue;
-            pos = (pos + S - 1) & ~(S - 1);
-            if (pos + S > T) continue;            // insert() returned false
-            for (uint32_t e = pos; e < pos + S; e++) sm.lut[e] = (uint16_t)(v | (w << 8));
-            pos += S;
-          }
-        }
-      }
-      // width-0 codes are never inserted (huffman.rs:163-165); anything left
-      // unfilled is an Absent tree node
-      if (pos != T) holes = 1;
-      sm.n = n;
-    }
-    sm.status = st;
-    sm.p = p;
-    sm.holes = holes;
+    lut[e] = (uint16_t)(LUT_ABSENT | ((uint32_t)(p - k) << 8));
   }
-  __syncthreads();
-  const int st = sm.status, p = sm.p;
-  if (st) {
-    if (lane == 0) {
-      uint32_t ph = (st == ZD_E_OUT_OF_DOMAIN) ? PH_LIMIT : PH_PARSE;
-      key_min(fstate, C.frame, make_key(ph, C.block_in_frame, PS_HUF_DESC, 0, st));
+}
+
+// HuffmanDecoder::parse + from_weights + from_number_of_bits (huffman.rs:
+// 80-203) -> LUT of 2^p u16 entries {symbol | width << 8}; entries no code
+// reaches get LUT_ABSENT | depth of the absent tree node.  Returns status;
+// *p_out = maxBits.
+__device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, K1Lane& L,
+                               uint16_t* lut, int* p_out) {
+  int st = 0;
+  uint32_t nw = 0;
+  const uint8_t h = desc[0];
+  if (h < 128) {
+    // parse_fse (huffman.rs:108-130): two alternating FSE states share one table
+    FwBits fw{desc + 1, h, 0};
+    uint8_t al;
+    uint32_t nsym;
+    st = parse_ncount(fw, &al, L.dist, &nsym);
+    if (!st) st = build_fse(al, L.dist, nsym, L.fse, L.sym, L.next);
+    BwBits bs;
+    if (!st) st = bs.init(desc + 1 + fw.bytes_read(), h - fw.bytes_read(), src, src_end);
+    if (!st) {
+      uint32_t sa = 0, sb = 0, v;
+      st = bs.take(al, &sa);
+      if (!st) st = bs.take(al, &sb);
+      bool last_updated_is_first = false, last_read_is_first = false;
+      bool has_a = true, has_b = true;
+      while (!st) {
+        const uint32_t cur = last_updated_is_first ? sb : sa;
+        const uint32_t nb = fse_nb(L.fse[cur], al);
+        if ((int64_t)nb > bs.bitpos) break;
+        uint32_t w;
+        if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
+        else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
+        if (nw >= K1_MAX_WEIGHTS - 2) { st = ZD_E_OUT_OF_DOMAIN; break; }
+        L.weights[nw++] = (uint8_t)w;
+        uint32_t& sx = last_updated_is_first ? sb : sa;
+        bool& has = last_updated_is_first ? has_b : has_a;
+        if (has) { st = ZD_E_REF_PANIC; break; }
+        st = bs.take((int)nb, &v);
+        if (st) break;
+        sx = fse_base(L.fse[sx], al) + v;
+        has = true;
+        last_updated_is_first = !last_updated_is_first;
+      }
+      for (int k = 0; k < 2 && !st; k++) {
+        uint32_t w;
+        if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
+        else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
+        L.weights[nw++] = (uint8_t)w;
+      }
     }
-    return;
+  } else {
+    // parse_direct (huffman.rs:92-106): high nibble first
+    nw = (uint32_t)h - 127;
+    for (uint32_t i = 0; i < nw; i++) {
+      const uint8_t b = desc[1 + i / 2];
+      L.weights[i] = (i & 1) ? (b & 15) : (b >> 4);
+    }
+  }
+  if (st) return st;
+  // from_weights (huffman.rs:177-203)
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < nw; i++) {
+    const uint32_t w = L.weights[i];
+    if (!w) continue;
+    if (w - 1 >= 32) return ZD_E_REF_PANIC;
+    const uint32_t add = 1u << (w - 1);
+    if (sum > 0xFFFFFFFFu - add) return ZD_E_REF_PANIC;
+    sum += add;
+  }
+  if (sum == 0) return ZD_E_REF_PANIC;
+  int p = highbit32(sum);
+  if ((1ull << p) < sum) p++;
+  if (p >= 32) return ZD_E_REF_PANIC;
+  const uint8_t rest = (uint8_t)((1u << p) - sum);
+  if (rest == 0) return ZD_E_REF_PANIC;           // D3
+  const uint32_t manquant = (uint32_t)highbit32(rest) + 1;
+  for (uint32_t i = 0; i < nw; i++)
+    if (L.weights[i] > (uint32_t)p + 1) return ZD_E_REF_PANIC;
+  if (manquant > (uint32_t)p + 1) return ZD_E_REF_PANIC;
+  if (p > LUT_MAX_BITS) return ZD_E_OUT_OF_DOMAIN;
+  L.weights[nw] = (uint8_t)manquant;          // the implied last symbol: width p + 1 - manquant
+  const uint32_t n = nw + 1;
+  // width(i) = weight ? p + 1 - weight : 0 (never inserted, huffman.rs:163-165)
+  // from_number_of_bits + insert (huffman.rs:132-175): longest codes first,
+  // ascending symbol, each at the leftmost free aligned slot; a code that no
+  // longer fits is not inserted.  Counting sort by width.
+  for (int w = 0; w <= p; w++) { L.cnt[w] = 0; L.placed[w] = 0; }
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t wt = L.weights[i];
+    if (wt) L.cnt[p + 1 - wt]++;
   }
   const uint32_t T = 1u << p;
-  if (sm.holes) {
-    // absent tree nodes: depth of the Absent node on each unfilled index's path
-    if (lane == 0) {
-      uint32_t c = 0;
-      for (uint32_t e = 0; e < T; e++) { sm.prefix[e] = (uint16_t)c; c += sm.lut[e] != 0xFFFF; }
-      sm.prefix[T] = (uint16_t)c;
-    }
-    __syncthreads();
-    for (uint32_t e = lane; e < T; e += 64) {
-      if (sm.lut[e] != 0xFFFF) continue;
-      int d = 0;
-      for (; d <= p; d++) {
-        uint32_t lo = (e >> (p - d)) << (p - d), hi = lo + (1u << (p - d));
-        if (sm.prefix[hi] == sm.prefix[lo]) break;
-      }
-      sm.lut[e] = (uint16_t)(LUT_ABSENT | (d << 8));
-    }
-    __syncthreads();
+  uint32_t pos = 0;
+  for (int w = p; w >= 1; w--) {
+    if (!L.cnt[w]) continue;
+    const uint32_t S = 1u << (p - w);
+    const uint32_t al = (pos + S - 1) & ~(S - 1);
+    lut_holes(lut, p, pos, al);               // alignment gap: absent tree nodes
+    const uint32_t fit = (T - al) / S;
+    const uint32_t k = L.cnt[w] < fit ? L.cnt[w] : fit;
+    L.start[w] = (uint16_t)al;
+    L.placed[w] = (uint16_t)k;                // the first k symbols of this width get slots
+    pos = al + k * S;
   }
-  uint16_t* dst = luts + (uint64_t)C.lut_slot * LUT_ENTRIES;
-  for (uint32_t e = lane; e < T; e += 64) dst[e] = sm.lut[e];
-  if (lane == 0) cstate[ci].huf_bits = (uint8_t)p;
+  lut_holes(lut, p, pos, T);
+  for (int w = 0; w <= p; w++) L.cnt[w] = 0;  // reused as rank counters
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t wt = L.weights[i];
+    if (!wt) continue;
+    const int w = p + 1 - (int)wt;
+    const uint32_t r = L.cnt[w]++;
+    if (r >= L.placed[w]) continue;
+    const uint32_t S = 1u << (p - w);
+    const uint32_t at = L.start[w] + r * S;
+    const uint16_t ent = (uint16_t)((i & 0xFF) | ((uint32_t)w << 8));
+    if (S >= 4) {
+      const uint64_t e4 = (uint64_t)ent * 0x0001000100010001ull;
+      for (uint32_t e = 0; e < S; e += 4) *(uint64_t*)(lut + at + e) = e4;
+    } else {
+      for (uint32_t e = 0; e < S; e++) lut[at + e] = ent;
+    }
+  }
+  *p_out = p;
+  return 0;
 }
-
-// Sequence tables (sequences.rs:91-187): RLE bytes, FSE descriptions, predefined.
-__device__ void k1_sequences(const uint8_t* src, const CompBlock& C, uint32_t ci, CompState* cstate,
-                             FrameState* fstate, uint16_t* fses, K1Smem& sm) {
-  const int lane = threadIdx.x;
-  const uint8_t* blk = src + C.src;
-  uint16_t* slot = fses + (uint64_t)C.fse_slot * FSE_SLOT;
+// Sequence tables (sequences.rs:91-187) of one block: RLE bytes, FSE
+// descriptions and predefined distributions, in LL, OF, ML order, each
+// written as compact entries to the block's slot.  Returns status; *stage_sub
+// = table index of a failure (3: the empty-bitstream check).
+__device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, K1Lane& L, uint16_t* slot, uint8_t al_out[3],
+                                 uint32_t* bs_off, uint32_t* bs_size, int* sub) {
   uint32_t pos = C.seq_tables;
   for (int k = 0; k < 3; k++) {
-    int mode = C.modes[k];
-    if (lane == 0) {
-      int st = 0, al = 0;
-      if (mode == M_RLE) {
-        if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
-        else { sm.fse[0] = fse_entry(blk[pos], 1); pos++; }   // AL 0: nb 0, baseline 0
-      } else if (mode == M_FSE) {
-        if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
-        else {
-          FwBits fw{blk + pos, C.size - pos, 0};
-          uint8_t a;
-          uint32_t nsym;
-          st = parse_ncount(fw, &a, sm.dist, &nsym);
-          if (!st) st = build_fse(a, sm.dist, nsym, sm.fse, sm.sym, sm.next);
-          al = a;
-          pos += fw.bytes_read();
-        }
-      } else if (mode == M_PREDEFINED) {
-        const int16_t* d = k == 0 ? c_ll_default : (k == 1 ? c_of_default : c_ml_default);
-        uint32_t nsym = k == 0 ? 36 : (k == 1 ? 29 : 53);
-        al = k == 1 ? 5 : 6;
-        for (uint32_t s = 0; s < nsym; s++) sm.dist[s] = d[s];
-        st = build_fse(al, sm.dist, nsym, sm.fse, sm.sym, sm.next);
+    *sub = k;
+    const int mode = C.modes[k];
+    uint16_t* tab = slot + k * FSE_TAB;
+    int st = 0, al = 0;
+    if (mode == M_RLE) {
+      if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
+      else { tab[0] = fse_entry(blk[pos], 1); pos++; }   // AL 0: nb 0, baseline 0
+    } else if (mode == M_FSE) {
+      if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
+      else {
+        FwBits fw{blk + pos, C.size - pos, 0};
+        uint8_t a;
+        uint32_t nsym;
+        st = parse_ncount(fw, &a, L.dist, &nsym);
+        if (!st) st = build_fse(a, L.dist, nsym, tab, L.sym, L.next);
+        al = a;
+        pos += fw.bytes_read();
       }
-      sm.status = st;
-      sm.p = al;
+    } else if (mode == M_PREDEFINED) {
+      const int16_t* d = k == 0 ? c_ll_default : (k == 1 ? c_of_default : c_ml_default);
+      const uint32_t nsym = k == 0 ? 36 : (k == 1 ? 29 : 53);
+      al = k == 1 ? 5 : 6;
+      for (uint32_t x = 0; x < nsym; x++) L.dist[x] = d[x];
+      st = build_fse(al, L.dist, nsym, tab, L.sym, L.next);
     }
-    __syncthreads();
-    if (sm.status) {
-      if (lane == 0) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, k, sm.status));
-      return;
-    }
-    if (mode != M_REPEAT) {
-      uint32_t T = 1u << sm.p;
-      for (uint32_t e = lane; e < T; e += 64) slot[k * FSE_TAB + e] = sm.fse[e];
-      if (lane == 0) cstate[ci].al[k] = (uint8_t)sm.p;
-    }
-    __syncthreads();
+    if (st) return st;
+    if (mode != M_REPEAT) al_out[k] = (uint8_t)al;
   }
-  if (lane == 0) {
-    // seq.bitstream = input.slice(input.len()) (sequences.rs:72)
-    if (pos >= C.size) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, 3, ZD_E_EMPTY_SLICE));
-    cstate[ci].bs_off = pos;
-    cstate[ci].bs_size = pos < C.size ? C.size - pos : 0;
-  }
+  *sub = 3;
+  *bs_off = pos;                                  // seq.bitstream = input.slice(input.len()) (sequences.rs:72)
+  *bs_size = pos < C.size ? C.size - pos : 0;
+  return pos >= C.size ? ZD_E_EMPTY_SLICE : 0;
 }
 
-__global__ __launch_bounds__(64) void zd_k_tables(const uint8_t* __restrict__ src, uint64_t src_size,
-                                                  const CompBlock* __restrict__ comp, CompState* cstate,
-                                                  FrameState* fstate, const uint32_t* __restrict__ list,
-                                                  uint16_t* luts, uint16_t* fses) {
-  __shared__ K1Smem sm;
-  const uint32_t ci = list[blockIdx.x];
+__global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restrict__ src, uint64_t src_size,
+                                                        const CompBlock* __restrict__ comp, CompState* cstate,
+                                                        FrameState* fstate, const uint32_t* __restrict__ list,
+                                                        uint32_t n_list, uint16_t* luts, uint16_t* fses) {
+  __shared__ K1Lane lanes[K1_LANES];
+  const uint32_t li = blockIdx.x * K1_LANES + threadIdx.x;
+  if (li >= n_list) return;
+  K1Lane& L = lanes[threadIdx.x];
+  const uint32_t ci = list[li];
   const CompBlock C = comp[ci];
   if (C.prebuilt) return;
-  if (C.lit_type == LIT_COMPRESSED && C.host_stage > PS_HUF_DESC)
-    k1_huffman(src, src + src_size, C, ci, cstate, fstate, luts, sm);
-  __syncthreads();
-  if (C.nseq > 0 && C.host_stage > PS_SEQ_TABLES) k1_sequences(src, C, ci, cstate, fstate, fses, sm);
+  const uint8_t* blk = src + C.src;
+  if (C.lit_type == LIT_COMPRESSED && C.host_stage > PS_HUF_DESC) {
+    int p = 0;
+    const int st = k1_huffman_lane(blk + C.lit_data, src, src + src_size, L, luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
+    if (st) {
+      const uint32_t ph = (st == ZD_E_OUT_OF_DOMAIN) ? PH_LIMIT : PH_PARSE;
+      key_min(fstate, C.frame, make_key(ph, C.block_in_frame, PS_HUF_DESC, 0, st));
+      return;                                     // Block::parse stops at the literals section
+    }
+    cstate[ci].huf_bits = (uint8_t)p;
+  }
+  if (C.nseq > 0 && C.host_stage > PS_SEQ_TABLES) {
+    uint8_t al[3] = {0, 0, 0};
+    uint32_t bo = 0, bsz = 0;
+    int sub = 0;
+    const int st = k1_sequences_lane(blk, C, L, fses + (uint64_t)C.fse_slot * FSE_SLOT, al, &bo, &bsz, &sub);
+    for (int k = 0; k < 3; k++)
+      if (C.modes[k] != M_REPEAT && (sub > k || !st)) cstate[ci].al[k] = al[k];
+    cstate[ci].bs_off = bo;
+    cstate[ci].bs_size = bsz;
+    if (st) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, (uint32_t)sub, st));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -502,6 +496,35 @@ __device__ inline uint32_t take_top(uint64_t& t, uint32_t k) {
   const uint32_t v = (uint32_t)((t >> 1) >> (63 - k));
   t <<= k;
   return v;
+}
+
+// Byte-aligned window: 16 bytes loaded at an unaligned address ending at
+// the byte that holds bit pos-1 (gfx950 runs HSA queues in unaligned access
+// mode, so global_load_dwordx4 takes any byte address), clamped at the input
+// base.  sh = 128 - (pos - window start) is then in [0, 31] (0..7 unless
+// clamped), so the top 64 bits below pos are one funnel with no edge cases.
+struct WinU {
+  uint64_t w0, w1;
+  uint32_t sh;
+};
+typedef uint64_t u64x2a1 __attribute__((ext_vector_type(2), aligned(1)));
+typedef __attribute__((address_space(1))) const u64x2a1 g_u64x2a1;
+__device__ inline WinU winu_load(const uint8_t* s, uintptr_t base, int32_t pos) {
+  const int32_t tb = (pos + 7) >> 3;
+  uintptr_t a = (uintptr_t)((intptr_t)s + tb - 16);
+  a = a < base ? base : a;
+  const u64x2a1 v = *(g_u64x2a1*)a;
+  WinU w;
+  w.w0 = v.x;
+  w.w1 = v.y;
+  w.sh = (uint32_t)((int32_t)(((intptr_t)a + 16 - (intptr_t)s) * 8) - pos);
+  return w;
+}
+// top 64 bits below pos - d (d + sh <= 94)
+__device__ inline uint64_t winu_top(const WinU& w, uint32_t d) {
+  const uint32_t k = w.sh + d;
+  const uint64_t f = (w.w1 << (k & 63)) | ((w.w0 >> 1) >> ((63 - k) & 63));
+  return k < 64 ? f : (w.w0 << (k & 63));
 }
 
 // ---------------------------------------------------------------------------
@@ -663,20 +686,20 @@ static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
 // Runs one block's sequences; TP is an LDS (lds_u16*) or HBM (g_u16*) table
 // pointer.  Returns 0 or the reference's error.
 template <typename TP>
-__device__ int seq_block(const uint8_t* bs, uint32_t bs_size, uintptr_t lo, TP tll, TP tml, TP tof, int all,
+__device__ int seq_block(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
                          int alo, int alm, uint32_t n, uint64_t* __restrict__ out, uint32_t rep[3]) {
   // BackwardBitParser::new (parsing.rs:200-220)
   if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
   const uint8_t lastb = bs[bs_size - 1];
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
-  Win w = win_load(bs, lo, pos);
+  WinU w = winu_load(bs, base, pos);
   // SequenceDecoder::initialize: LL, OF, ML (sequence.rs:59-65)
   if (all + alo + alm > pos) return ZD_E_NOT_ENOUGH_BITS;
-  uint64_t t0 = win_top(w, pos);
+  uint64_t t0 = winu_top(w, 0);
   uint32_t sLL = take_top(t0, all), sOF = take_top(t0, alo), sML = take_top(t0, alm);
   pos -= all + alo + alm;
-  w = win_load(bs, lo, pos);
+  w = winu_load(bs, base, pos);
   // consume the first window here, so the loop head's wait covers only the
   // latch's load (vmcnt(1): the step's store may stay in flight)
   asm volatile("" : "+v"(w.w0), "+v"(w.w1));
@@ -698,17 +721,17 @@ __device__ int seq_block(const uint8_t* bs, uint32_t bs_size, uintptr_t lo, TP t
     ml_code(mlc, &mlbase, &mlb);
     const uint32_t nsL = eLL >> 6, nsM = eML >> 6, nsO = eOF >> 6;
     const uint32_t nbL = __clz(nsL) + aL, nbM = __clz(nsM) + aM, nbO = __clz(nsO) + aO;
-    const int32_t E = (int32_t)((ofc & 31) + mlb + llb);
+    const uint32_t E = (ofc & 31) + mlb + llb;
     const bool last = i + 1 == n;
-    const int32_t S = last ? 0 : (int32_t)(nbL + nbM + nbO);
-    st = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : (E + S > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
+    const uint32_t S = last ? 0 : nbL + nbM + nbO;
+    st = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : ((int32_t)(E + S) > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
     // every use of this step's window precedes the next window's load, and
     // the load precedes this step's store: the next step waits on the load only
-    uint64_t t = win_top(w, pos);
-    uint64_t t2 = win_top(w, pos - E);
-    pos -= E + S;
+    uint64_t t = winu_top(w, 0);
+    uint64_t t2 = winu_top(w, E);
+    pos -= (int32_t)(E + S);
     asm volatile("" : "+v"(t), "+v"(t2)::"memory");   // the window's reads stay above its reload
-    w = win_load(bs, lo, pos);
+    w = winu_load(bs, base, pos);
     // update_symbol_value (sequence.rs:41-55): OF, ML, LL extra bits
     const uint32_t ob = take_top(t, ofc & 31), mb = take_top(t, mlb), lb = take_top(t, llb);
     const uint32_t ofv = (1u << (ofc & 31)) + ob, ml = mlbase + mb, ll = llbase + lb;
@@ -772,7 +795,7 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
   if (!act) return;
   const CompState cs = cstate[ci];
   const uint8_t* blk = src + C.src;
-  const uintptr_t lo = (uintptr_t)blk & ~(uintptr_t)3;
+  const uintptr_t lo = (uintptr_t)src;
   uint32_t rep[3];
   rep_init(rep);
   int st;
@@ -1068,8 +1091,8 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   hipError_t e;
   if (a.events) if ((e = hipEventRecord(a.events[0], s)) != hipSuccess) return e;
   if (a.n_tables)
-    hipLaunchKernelGGL(zd_k_tables, dim3(a.n_tables), dim3(64), 0, s, a.src, a.src_size, comp, cstate, fstate,
-                       (const uint32_t*)(ws + W.list_tables), luts, fses);
+    hipLaunchKernelGGL(zd_k_tables, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
+                       a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
   if (a.n_huf)
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s, a.src, comp,
