@@ -23,9 +23,13 @@ def gpu(data, p=False):
     return decompress_status(data, p)
 
 
-def assert_parity(data, p=False, what=""):
+def assert_parity(data, p=False, what="", allow_ood=False):
+    """allow_ood: the input may leave the GPU path's domain (corrupted input
+    decoding past its declared content size)."""
     ost, oout = oracle.decompress_status(data, p)
     gst, gout = gpu(data, p)
+    if allow_ood and gst == OUT_OF_DOMAIN:
+        return ost, gst
     if ost == 0:
         assert gst == 0, f"{what}: oracle ok, gpu status {gst}"
         assert gout == oout, f"{what}: output differs (len {len(gout)} vs {len(oout)})"
@@ -163,7 +167,7 @@ def test_corrupted_inputs():
             d[r.randrange(len(d))] = r.randrange(256)
         if r.random() < 0.2:
             d = d[: r.randrange(len(d))]
-        ost, gst = assert_parity(bytes(d), False, f"corrupt #{it}")
+        ost, gst = assert_parity(bytes(d), False, f"corrupt #{it}", allow_ood=True)
         stats["ok" if ost == 0 else ("ood" if gst == OUT_OF_DOMAIN else "err_same")] += 1
     assert stats["ok"] + stats["err_same"] >= 290, stats
 

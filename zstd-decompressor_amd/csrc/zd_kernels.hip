@@ -649,18 +649,42 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     if (st) key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, k, st));
   }
   __syncthreads();
+  // The reference concatenates what each stream decodes until it runs out of
+  // bits (literals.rs:68-81).  When a block's streams do not hold their RFC
+  // shares (only in non-conforming input), lane 0 lays the streams out
+  // back-to-back and the block's lanes decode again into that layout.
+  __shared__ uint32_t redo_at[K2_BLOCKS][4];
+  __shared__ int redo[K2_BLOCKS];
   if (act && k == 0) {
-    bool err = false, ood = false;
+    bool err = false, rfc = true;
     for (int j = 0; j < m; j++) err |= errs[b][j] != 0;
     uint32_t total = 0;
     for (int j = 0; j < m && !err; j++) {
       const uint32_t cap = j < m - 1 ? seg : (R > (uint32_t)j * seg ? R - (uint32_t)j * seg : 0);
-      if (j < m - 1 ? counts[b][j] != seg : counts[b][j] > cap) ood = true;
+      if (j < m - 1 ? counts[b][j] != seg : counts[b][j] > cap) rfc = false;
+      redo_at[b][j] = total;
       total += counts[b][j];
     }
-    if (ood && !err) key_min(fstate, C.frame, make_key(PH_LIMIT, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
+    const bool fits = total <= R + 16;          // the block's literal slot (host: R + 16 bytes)
+    if (!rfc && !err && !fits)
+      key_min(fstate, C.frame, make_key(PH_LIMIT, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
+    redo[b] = !rfc && !err && fits;
     cstate[ci].lit_count = total;
-    if (err || ood) cstate[ci].stop = 1;
+    if (err || (!rfc && !fits)) cstate[ci].stop = 1;
+  }
+  __syncthreads();
+  if (act && k < m && redo[b]) {
+    uint32_t off = C.streams;
+    for (int j = 0; j < k; j++) off += C.stream_size[j];
+    const uint8_t* blk = src + C.src;
+    uint32_t count;
+    const uint32_t at = redo_at[b][k];
+    if (use_lds)
+      (void)huf_stream<const lds_u16*>(blk + off, C.stream_size[k], (uintptr_t)blk & ~(uintptr_t)3,
+                                       (const lds_u16*)lut[b], p, lits + C.lit_out + at, counts[b][k], &count);
+    else
+      (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)blk & ~(uintptr_t)3, (g_u16*)g, p,
+                               lits + C.lit_out + at, counts[b][k], &count);
   }
 }
 
@@ -678,7 +702,10 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
 // zstd, whose offset tables are AL <= 8) makes its workgroup read tables from
 // HBM instead.
 // ---------------------------------------------------------------------------
-constexpr int K3_LANES = 32;
+#ifndef ZD_K3_LANES
+#define ZD_K3_LANES 32
+#endif
+constexpr int K3_LANES = ZD_K3_LANES;
 constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
 static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
@@ -816,12 +843,50 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
 }
 
 // ---------------------------------------------------------------------------
-// K4: execute
+// K4: execute (decoding_context.rs:50-106 + block.rs:74-99), one frame per
+// wave, one sequence per lane, 64 sequences per batch.  A frame that decodes
+// past the capacity its plan reserved (its Frame_Content_Size, or 128 KiB per
+// block without one; the reference checks neither) is out of the GPU path's
+// domain (ZD_E_OUT_OF_DOMAIN).
+//
+// The wave keeps a linear LDS window: frame bytes [hs, pos) with hs aligned
+// so that LDS offsets and HBM addresses share 16-byte alignment.  A batch
+// writes its literals and matches into the window with 16-byte unaligned LDS
+// copies (gfx950 runs in unaligned mode; tools/unaligned_check.hip), then the
+// completed aligned chunks are flushed to HBM with 16-byte stores, and every
+// K4_B bytes the last K4_W bytes slide to the front.  Match sources before
+// hs are read from the frame's output in HBM (L1-bypassing loads, after the
+// flush stores have drained).  Matches may depend on earlier sequences of
+// the same batch: a lane copies once its source lies entirely below the
+// first unfinished sequence's match (the batch frontier); a match copies its
+// source period by period, byte q+j = byte q-off+(j mod off), which is the
+// reference's byte-by-byte push (decoding_context.rs:95-98).
 // ---------------------------------------------------------------------------
-constexpr int RING = 8192;
-constexpr uint32_t RMASK = RING - 1;
-constexpr uint32_t BATCH = 2048;
+constexpr int K4_W = 4096;                    // history kept after a slide
+constexpr int K4_B = 4096;                    // room for a batch
+constexpr int K4_C = K4_W + K4_B + 32;        // window bytes
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(3))) uint8_t l_u8;
+typedef __attribute__((address_space(3))) u32x4a1 l_u32x4a1;
+typedef __attribute__((address_space(3))) uint64_t l_u64a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint32_t l_u32a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint16_t l_u16a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4a1 g_cu32x4a1;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 
+__device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
+__device__ inline u32x4 ldg16_nt(const uint8_t* p) { return __builtin_nontemporal_load((g_cu32x4a1*)p); }
+__device__ inline u32x4 lds16(const l_u8* p) { return *(const l_u32x4a1*)p; }
+// stores the first n (0..16) bytes of v at p
+__device__ inline void sts_n(l_u8* p, u32x4 v, uint32_t n) {
+  if (n >= 16) { *(l_u32x4a1*)p = v; return; }
+  if (n & 8) { *(l_u64a1*)p = (uint64_t)v.x | ((uint64_t)v.y << 32); v.x = v.z; v.y = v.w; p += 8; }
+  if (n & 4) { *(l_u32a1*)p = v.x; v.x = v.y; p += 4; }
+  if (n & 2) { *(l_u16a1*)p = (uint16_t)v.x; v.x >>= 16; p += 2; }
+  if (n & 1) { *p = (uint8_t)v.x; }
+}
+__device__ inline void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ inline int64_t readlane_i64(int64_t x, int l) {
   int lo = __shfl((int)(uint32_t)x, l, 64);
   int hi = __shfl((int)(uint32_t)((uint64_t)x >> 32), l, 64);
@@ -835,51 +900,126 @@ __device__ inline uint32_t scan_incl_u32(uint32_t x, int lane) {
   return x;
 }
 
-struct Exec {
-  uint8_t* ring;
-  uint8_t* out;          // frame output position 0
-  uintptr_t out_abs;
-  uint64_t pos;          // frame-relative decoded length
-  uint64_t frontier;     // bytes [0, frontier) are in HBM
-  uint64_t cap;
+struct K4 {
+  l_u8* buf;
+  uint8_t* out;            // frame output (frame position 0)
+  intptr_t oabs;
+  int64_t hs;              // frame position of buf[0]; (oabs + hs) % 16 == 0
+  int64_t pos;             // decoded length
+  int64_t fl;              // HBM holds [0, fl)
+  int64_t cap;
   int lane;
-
-  __device__ inline uint8_t& R(uint64_t p) { return ring[(out_abs + p) & RMASK]; }
-
-  // aligned 16-B stores of the completed chunks; the frame's head chunk by bytes
-  __device__ void flush() {
-    uintptr_t A = out_abs + frontier, E = out_abs + pos;
-    uintptr_t c0 = A & ~(uintptr_t)15, c1 = E & ~(uintptr_t)15;
-    for (uintptr_t c = c0 + 16 * (uintptr_t)lane; c < c1; c += 16 * 64) {
-      if (c >= out_abs) {
-        *(uint4*)c = *(const uint4*)&ring[c & RMASK];
-      } else {
-        for (uintptr_t b = out_abs; b < c + 16; b++) *(uint8_t*)b = ring[b & RMASK];
-      }
-    }
-    if (c1 > A) frontier = c1 - out_abs;
-  }
-  __device__ void final_flush() {
-    uintptr_t A = out_abs + frontier, E = out_abs + pos;
-    for (uintptr_t b = A + lane; b < E; b += 64) *(uint8_t*)b = ring[b & RMASK];
-    frontier = pos;
-  }
-  // append n bytes from s (or the fill byte when s == nullptr), through the ring
-  __device__ bool emit(const uint8_t* s, uint8_t fill, uint64_t n) {
-    for (uint64_t done = 0; done < n;) {
-      uint32_t chunk = (uint32_t)min((uint64_t)BATCH, n - done);
-      if (pos + chunk > cap) return false;
-      for (uint32_t x = lane; x < chunk; x += 64) R(pos + x) = s ? s[done + x] : fill;
-      __syncthreads();
-      pos += chunk;
-      done += chunk;
-      flush();
-    }
-    return true;
-  }
+  __device__ inline l_u8* at(int64_t p) const { return buf + (p - hs); }
+  __device__ inline int64_t space() const { return K4_C - (pos - hs); }
+  // 16 bytes of frame output at p (p >= 0): LDS when inside the window, else HBM
+  __device__ inline u32x4 src16(int64_t p) const { return p >= hs ? lds16(at(p)) : ldg16_nt(out + p); }
 };
 
-__device__ inline void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// HBM <- window: the aligned 16-byte chunks of [fl, pos) (all of it if final)
+__device__ void k4_flush(K4& X, bool final) {
+  const intptr_t A = (X.oabs + X.fl) & ~(intptr_t)15, E = (X.oabs + X.pos) & ~(intptr_t)15;
+  for (intptr_t c = A + 16 * X.lane; c < E; c += 1024) {
+    const u32x4 v = lds16(X.at(c - X.oabs));
+    if (c >= X.oabs) {
+      *(g_u32x4*)c = v;
+    } else {                                   // the frame's head chunk: only its own bytes
+      for (intptr_t b = X.oabs; b < c + 16; b++) *(uint8_t*)b = *X.at(b - X.oabs);
+    }
+  }
+  if (final) {
+    const intptr_t lo = E > X.oabs + X.fl ? E : X.oabs + X.fl;
+    for (intptr_t b = lo + X.lane; b < X.oabs + X.pos; b += 64) *(uint8_t*)b = *X.at(b - X.oabs);
+    X.fl = X.pos;
+  } else if (E - X.oabs > X.fl) {
+    X.fl = E - X.oabs;
+  }
+}
+
+// Slides the window so that at least K4_B - 16 bytes are free (keeps K4_W of history).
+__device__ void k4_room(K4& X) {
+  if (X.space() >= K4_B) return;
+  const int64_t nh = ((X.oabs + X.pos - K4_W) & ~(intptr_t)15) - X.oabs;   // <= fl: pos - fl < 16
+  const int64_t n = X.pos - nh;                // <= K4_W + 15 bytes move down by nh - hs
+  constexpr int PER = (K4_W + 16 + 1023) / 1024;
+  u32x4 keep[PER];
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const int64_t x = 16 * X.lane + 1024 * r;
+    if (x < n) keep[r] = lds16(X.at(nh + x));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const int64_t x = 16 * X.lane + 1024 * r;
+    if (x < n) *(l_u32x4a1*)(X.buf + x) = keep[r];
+  }
+  __syncthreads();
+  X.hs = nh;
+}
+
+// Appends n literal bytes from s (HBM) or the fill byte (s == nullptr), the
+// whole wave copying 16 bytes per lane.  false: past the frame capacity.
+__device__ bool k4_emit_lits(K4& X, const uint8_t* s, uint32_t fill, uint64_t n) {
+  const u32x4 f4 = (u32x4){fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u};
+  while (n) {
+    k4_room(X);
+    const int64_t chunk = (int64_t)n < X.space() - 16 ? (int64_t)n : X.space() - 16;
+    if (X.pos + chunk > X.cap) return false;
+    for (int64_t x = 16 * X.lane; x < chunk; x += 1024) {
+      const u32x4 v = s ? ldg16(s + x) : f4;
+      sts_n(X.at(X.pos + x), v, (uint32_t)(chunk - x));
+    }
+    __syncthreads();
+    X.pos += chunk;
+    if (s) s += chunk;
+    n -= (uint64_t)chunk;
+    k4_flush(X, false);
+  }
+  return true;
+}
+
+// Appends n bytes of a match at offset off (1 <= off <= pos), whole wave.
+// Byte j = byte (q - off + j mod off): every source byte precedes the match
+// start q, in the window or (once slid out) in HBM.  A period shorter than 16
+// is first unrolled into `pat` (48 bytes of it), so every 16-byte piece is one
+// LDS read.
+__device__ bool k4_emit_match(K4& X, l_u8* pat, uint64_t off, uint64_t n) {
+  const int64_t q = X.pos;                     // match start
+  uint64_t j0 = 0;
+  const bool small = off < 16;
+  const bool need_hbm = !small && (int64_t)(q - (int64_t)off) < X.hs;
+  if (small) {                                 // q - off >= hs here: the period is in the window
+    if (X.lane < 48) pat[X.lane] = *X.at(q - (int64_t)off + (int64_t)((uint64_t)X.lane % off));
+    __syncthreads();
+  }
+  if (__ballot(need_hbm)) wait_vm();
+  while (j0 < n) {
+    k4_room(X);
+    if (j0 && !small) wait_vm();              // the last chunk's flush, before reading it back
+    const int64_t chunk = (int64_t)(n - j0) < X.space() - 16 ? (int64_t)(n - j0) : X.space() - 16;
+    if (X.pos + chunk > X.cap) return false;
+    for (int64_t x = 16 * X.lane; x < chunk; x += 1024) {
+      const uint64_t j = j0 + (uint64_t)x, r = j % off;
+      const uint32_t m = (uint32_t)(chunk - x < 16 ? chunk - x : 16);
+      if (small) {
+        sts_n(X.at(X.pos + x), lds16(pat + r), m);
+      } else if (r + m <= off) {
+        sts_n(X.at(X.pos + x), X.src16(q - (int64_t)off + (int64_t)r), m);
+      } else {                                 // the piece wraps at the period
+        for (uint32_t b = 0; b < m; b++) {
+          const uint64_t rb = (j + b) % off;
+          const int64_t p = q - (int64_t)off + (int64_t)rb;
+          *X.at(X.pos + x + b) = p >= X.hs ? *X.at(p) : __builtin_nontemporal_load(X.out + p);
+        }
+      }
+    }
+    __syncthreads();
+    X.pos += chunk;
+    j0 += (uint64_t)chunk;
+    k4_flush(X, false);
+  }
+  return true;
+}
 
 __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ src, uint8_t* outbase,
                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
@@ -888,8 +1028,8 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
                                                    const CompState* __restrict__ cstate,
                                                    const uint8_t* __restrict__ lits,
                                                    const uint64_t* __restrict__ seqs) {
-  __shared__ __attribute__((aligned(16))) uint8_t ring[RING];
-  __shared__ uint8_t stage[BATCH];
+  __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
+  __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   const int lane = threadIdx.x;
   const uint32_t f = blockIdx.x;
   const FrameDesc F = frames[f];
@@ -897,18 +1037,21 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
   const uint64_t key0 = S->key;
   if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
 
-  Exec X;
-  X.ring = ring;
+  K4 X;
+  X.buf = (l_u8*)win;
   X.out = outbase + F.out;
-  X.out_abs = (uintptr_t)X.out;
-  X.pos = F.out_len0;
-  X.frontier = F.out_len0;
-  X.cap = F.out_cap;
+  X.oabs = (intptr_t)X.out;
   X.lane = lane;
-  // context API: the window ring starts with the tail of the existing output
-  if (X.pos) {
-    uint64_t lo = X.pos > (uint64_t)RING ? X.pos - RING : 0;
-    for (uint64_t p = lo + lane; p < X.pos; p += 64) X.R(p) = X.out[p];
+  X.pos = (int64_t)F.out_len0;
+  X.fl = X.pos;
+  X.cap = (int64_t)F.out_cap;
+  {
+    // window start: aligned, at most K4_W bytes back (context API: the
+    // existing output's tail comes back from HBM)
+    const int64_t back = X.pos > K4_W ? X.pos - K4_W : 0;
+    X.hs = ((X.oabs + back) & ~(intptr_t)15) - X.oabs;
+    for (int64_t p = (X.hs > 0 ? X.hs : 0) + lane; p < X.pos; p += 64) *X.at(p) = X.out[p];
+    __syncthreads();
   }
   uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
   uint64_t err_key = KEY_NONE;
@@ -918,49 +1061,50 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
     if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
     if (B.type == 5) continue;
     if (B.type == 0 || B.type == 4) {
-      if (!X.emit(src + B.src, 0, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_DST_TOO_SMALL);
+      if (!k4_emit_lits(X, src + B.src, 0, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN);
       continue;
     }
     if (B.type == 1) {
-      if (!X.emit(nullptr, B.rle, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_DST_TOO_SMALL);
+      if (!k4_emit_lits(X, nullptr, B.rle, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN);
       continue;
     }
     const CompBlock C = comp[B.comp];
     const CompState CS = cstate[B.comp];
     if (CS.stop) break;
     const uint8_t* lsrc = nullptr;
-    uint8_t lfill = 0;
+    uint32_t lfill = 0;
     uint64_t nl;
     if (C.lit_type == LIT_RAW) { lsrc = src + C.src + C.lit_data; nl = C.lit_regen; }
     else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle; nl = C.lit_regen; }
     else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
+    const u32x4 f4 = (u32x4){lfill * 0x01010101u, lfill * 0x01010101u, lfill * 0x01010101u, lfill * 0x01010101u};
     uint64_t lit_cursor = 0;
     const uint64_t* SQ = seqs + C.seq_out;
     const uint32_t n = C.nseq;
+    uint64_t nxt = lane < (int)n ? SQ[lane] : 0;
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
       const uint32_t i = s0 + lane;
       const bool valid = i < n;
-      const uint64_t sq = valid ? SQ[i] : 0;
-      const uint32_t ll = seq_ll(sq), ml = seq_ml(sq);
+      const uint64_t sq = nxt;
+      nxt = (i + 64 < n) ? SQ[i + 64] : 0;       // next batch's records, in flight
+      const uint32_t ll = valid ? seq_ll(sq) : 0, ml = valid ? seq_ml(sq) : 0;
       // decode_offset (decoding_context.rs:50-75): K3's code against the block's incoming offsets
-      uint64_t offu = 0;
-      const int derr = valid ? off_resolve(seq_off(sq), rep, &offu) : 0;
-      const int64_t off = (int64_t)offu;
-      // positions
+      uint64_t off = 0;
+      const int derr = valid ? off_resolve(seq_off(sq), rep, &off) : 0;
+      k4_room(X);
       const uint32_t tot = ll + ml;
       const uint32_t inc_tot = scan_incl_u32(tot, lane);
       const uint32_t inc_ll = scan_incl_u32(ll, lane);
       const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
       // checks (decoding_context.rs:86-90, D9)
-      const uint64_t before = X.pos + opos;
+      const uint64_t before = (uint64_t)X.pos + opos;
       const bool dbad = valid && derr != 0;
       const bool imp = valid && !dbad && ((uint64_t)ll > nl - (lit_cursor + lpos) || lit_cursor + lpos > nl ||
-                                          offu > before + ll);
-      const bool panic = valid && !dbad && !imp && ml != 0 && offu == 0;
+                                          off > before + ll);
+      const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
       const uint64_t badm = __ballot(dbad || imp || panic);
-      // batch: sequences whose bytes fit in BATCH
-      const uint64_t fitm = __ballot(valid && inc_tot <= BATCH);
-      uint32_t k = (uint32_t)__popcll(fitm);
+      const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= X.space() - 16);
+      const uint32_t k = (uint32_t)__popcll(fitm);
       if (badm) {
         const int b = __ffsll((long long)badm) - 1;
         if ((uint32_t)b < (k ? k : 1u)) {
@@ -969,92 +1113,84 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
           break;
         }
       }
-      if (k > 0) {
-        // ---- small path: lanes < k ----
-        const uint32_t T = __shfl(inc_tot, k - 1, 64);
-        const uint32_t L = __shfl(inc_ll, k - 1, 64);
-        if (X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_DST_TOO_SMALL); break; }
-        for (uint32_t x = lane; x < L; x += 64) stage[x] = lsrc ? lsrc[lit_cursor + x] : lfill;
-        __syncthreads();
-        const bool act = (uint32_t)lane < k;
-        if (act) for (uint32_t x = 0; x < ll; x++) X.R(X.pos + opos + x) = stage[lpos + x];
-        // matches
-        const uint64_t q = X.pos + opos + ll;
-        const uint64_t batch_end = X.pos + T;
-        const uint64_t ring_lo = batch_end > (uint64_t)RING ? batch_end - RING : 0;
-        const uint64_t slo = act && ml ? q - (uint64_t)off : 0;
-        const uint64_t shi = act && ml ? slo + min((uint64_t)off, (uint64_t)ml) : 0;
-        if (__ballot(act && ml && slo < ring_lo)) wait_vm();
-        uint64_t done = __ballot(!act || ml == 0);
-        __syncthreads();
-        while (done != ~0ull) {
-          const int U = __ffsll((long long)~done) - 1;
-          const uint64_t qU = (uint64_t)readlane_i64((int64_t)q, U);
-          const bool mine = !((done >> lane) & 1) && (lane == U || shi <= qU);
-          if (mine) {
-            uint64_t p = slo;
-            for (uint32_t x = 0; x < ml; x++) {
-              uint8_t byte = p >= ring_lo ? X.R(p) : X.out[p];
-              X.R(q + x) = byte;
-              p++;
-              if (p == q) p = slo;
-            }
-          }
-          done |= __ballot(mine);
-          __syncthreads();
-        }
-        // advance
-        lit_cursor += L;
-        X.pos += T;
-        s0 += k;
-        X.flush();
-      } else {
-        // ---- big path: lane 0's sequence alone ----
+      if (k == 0) {
+        // one sequence larger than the window's room: the whole wave copies it
         const uint32_t ll0 = __shfl(ll, 0, 64), ml0 = __shfl(ml, 0, 64);
-        const uint64_t off0 = (uint64_t)readlane_i64(off, 0);
-        if (!X.emit(lsrc ? lsrc + lit_cursor : nullptr, lfill, ll0)) {
-          err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_DST_TOO_SMALL);
+        const uint64_t off0 = (uint64_t)readlane_i64((int64_t)off, 0);
+        if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, ll0) || !k4_emit_match(X, (l_u8*)pat, off0, ml0)) {
+          err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN);
           break;
         }
         lit_cursor += ll0;
-        for (uint32_t k0 = 0; k0 < ml0;) {
-          const uint32_t P = min(BATCH, ml0 - k0);
-          if (X.pos + P > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_DST_TOO_SMALL); break; }
-          const uint64_t ps = X.pos;
-          const uint64_t ring_lo = ps + P > (uint64_t)RING ? ps + P - RING : 0;
-          const uint64_t lowest = ps > off0 ? ps - off0 : 0;
-          if (lowest < ring_lo) wait_vm();
-          for (uint32_t x = lane; x < P; x += 64) {
-            const uint64_t m = off0 > P ? 0 : x / (uint32_t)off0;
-            const uint64_t p = ps + x - off0 * (m + 1);
-            X.R(ps + x) = p >= ring_lo ? X.R(p) : X.out[p];
-          }
-          __syncthreads();
-          X.pos += P;
-          k0 += P;
-          X.flush();
-        }
         s0 += 1;
+        if (s0 < n) nxt = (s0 + lane < n) ? SQ[s0 + lane] : 0;
+        continue;
       }
+      const uint32_t T = __shfl(inc_tot, k - 1, 64);
+      const uint32_t L = __shfl(inc_ll, k - 1, 64);
+      if (X.pos + (int64_t)T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN); break; }
+      const bool act = (uint32_t)lane < k;
+      // literals (every lane its own run)
+      if (act && ll) {
+        l_u8* d = X.at(X.pos + opos);
+        for (uint32_t x = 0; x < ll; x += 16) {
+          const u32x4 v = lsrc ? ldg16(lsrc + lit_cursor + lpos + x) : f4;
+          sts_n(d + x, v, ll - x);
+        }
+      }
+      // matches, in frontier rounds
+      const int64_t q = X.pos + opos + ll;
+      const int64_t slo = q - (int64_t)off;
+      const int64_t shi = slo + (int64_t)(off < ml ? off : ml);
+      if (__ballot(act && ml && slo < X.hs)) wait_vm();
+      uint64_t done = __ballot(!act || ml == 0);
+      __syncthreads();
+      while (done != ~0ull) {
+        const int U = __ffsll((long long)~done) - 1;
+        const int64_t qU = readlane_i64(q, U);
+        const bool mine = !((done >> lane) & 1) && (lane == U || shi <= qU);
+        if (mine) {
+          l_u8* d = X.at(q);
+          if (off >= 16) {
+            for (uint32_t x = 0; x < ml; x += 16) sts_n(d + x, X.src16(slo + x), ml - x);
+          } else {                             // small period: first 16 bytes bytewise, then 16-byte steps
+            const uint32_t m16 = (uint32_t)off * ((16 + (uint32_t)off - 1) / (uint32_t)off);
+            const uint32_t head = ml < 16 ? ml : 16;
+            uint32_t r = 0;
+            for (uint32_t x = 0; x < head; x++) {
+              d[x] = *X.at(slo + r);
+              r = r + 1 == off ? 0 : r + 1;
+            }
+            for (uint32_t x = 16; x < ml; x += 16) sts_n(d + x, lds16(d + x - m16), ml - x);
+          }
+        }
+        done |= __ballot(mine);
+        __syncthreads();
+      }
+      lit_cursor += L;
+      X.pos += T;
+      s0 += k;
+      if (k < 64 && s0 < n) nxt = (s0 + lane < n) ? SQ[s0 + lane] : 0;
+      k4_flush(X, false);
     }
     if (err_key != KEY_NONE) break;
     // repeat offsets after the block
     if (n) {
       uint64_t nr[3];
-      for (int k = 0; k < 3; k++) (void)off_resolve(CS.rep_out[k], rep, &nr[k]);
+      for (int kk = 0; kk < 3; kk++) (void)off_resolve(CS.rep_out[kk], rep, &nr[kk]);
       rep[0] = nr[0]; rep[1] = nr[1]; rep[2] = nr[2];
     }
     // leftover literals (decoding_context.rs:101-103)
-    if (lit_cursor < nl && !X.emit(lsrc ? lsrc + lit_cursor : nullptr, lfill, nl - lit_cursor))
-      err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_DST_TOO_SMALL);
+    if (lit_cursor < nl && !k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, nl - lit_cursor))
+      err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_OUT_OF_DOMAIN);
   }
   if (err_key != KEY_NONE) {
     if (lane == 0) key_min(fstate, f, err_key);
     return;
   }
-  X.final_flush();
+  k4_flush(X, true);
   if (lane == 0) {
-    S->out_len = X.pos;
+    S->out_len = (uint64_t)X.pos;
     S->rep[0] = rep[0];
     S->rep[1] = rep[1];
     S->rep[2] = rep[2];

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libzd.so")
+LIB_PATH = os.environ.get("ZD_LIB_PATH") or os.path.join(_PKG, "lib", "libzd.so")
 
 # status codes (include/zd.h)
 OK = 0
