@@ -459,37 +459,6 @@ typedef __attribute__((address_space(1))) const u32x4a4 g_u32x4a4;   // global (
 typedef __attribute__((address_space(3))) uint16_t lds_u16;          // LDS tables
 typedef __attribute__((address_space(1))) const uint16_t g_u16;      // HBM tables
 
-// 16 bytes at a 4-aligned address ending at or after the byte holding bit
-// pos-1 of the stream at s; `bit` = stream bit index of w0's bit 0.  The
-// window covers at least 97 bits below pos (>= the 90 bits one sequence can
-// consume: 63 extra + 27 state bits).
-struct Win {
-  uint64_t w0, w1;
-  int32_t bit;
-};
-__device__ inline Win win_load(const uint8_t* s, uintptr_t lo, int32_t pos) {
-  // branch-free: a = max(lo, align_up(top - 16, 4)); pos may be slightly
-  // negative after a failing step, which also clamps to lo
-  const intptr_t top = (intptr_t)s + ((pos + 7) >> 3);
-  uintptr_t a = (uintptr_t)(top - 13) & ~(uintptr_t)3;
-  a = a < lo ? lo : a;
-  u32x4a4 v = *(g_u32x4a4*)a;
-  Win w;
-  w.w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
-  w.w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-  w.bit = (int32_t)((intptr_t)a - (intptr_t)s) * 8;
-  return w;
-}
-// bits [r-64, r) of the 128-bit window, r = pos - bit in [0, 128]; branch-free
-// (64-bit shifts on gfx950 take the amount mod 64, so the edges are selects)
-__device__ inline uint64_t win_top(const Win& w, int32_t pos) {
-  const int r = pos - w.bit;
-  const int sh = r - 64;                             // >= 0: funnel of w1:w0
-  const uint64_t f_lo = sh >= 64 ? 0 : (w.w0 >> (sh & 63));
-  const uint64_t f_hi = sh <= 0 ? 0 : (w.w1 << ((64 - sh) & 63));
-  const uint64_t low = r <= 0 ? 0 : (w.w0 << ((64 - r) & 63));
-  return sh >= 0 ? (f_lo | f_hi) : low;
-}
 // MSB-first field of k bits from the top of t, k in [0, 63], no selects:
 // (t >> 1) >> (63 - k) is 0 for k = 0.
 __device__ inline uint32_t take_top(uint64_t& t, uint32_t k) {
@@ -544,10 +513,17 @@ constexpr int K2_LUT_BITS = 11;
 constexpr int K2_GROUP = 8;
 static_assert(K2_LANES <= 64, "K2 workgroup must be a single wave");
 static_assert(K2_GROUP * LUT_MAX_BITS <= 97, "a group must fit one window");
+static_assert((K2_GROUP / 2) * LUT_MAX_BITS <= 64, "half a group must fit 64 bits");
 typedef __attribute__((address_space(1))) uint64_t g_u64a1 __attribute__((aligned(1)));
 
+// One Huffman stream, backward (huffman.rs:205-218 on a BackwardBitParser,
+// parsing.rs:191-259).  Fast path while at least K2_GROUP * 12 bits remain:
+// a byte-aligned 16-byte window per group of 8 symbols, the top 64 bits
+// taken twice (4 symbols each, <= 48 bits), one LDS lookup and one shift per
+// symbol, one 8-byte store per group.  The tail (and any group that meets an
+// absent tree node) goes symbol by symbol with the reference's checks.
 template <typename LP>
-__device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t lo, LP lut, int p, uint8_t* out,
+__device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP lut, int p, uint8_t* out,
                           uint32_t cap, uint32_t* count_out) {
   uint32_t count = 0;
   *count_out = 0;
@@ -555,34 +531,43 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t lo, LP lut
   const uint8_t lastb = bs[size - 1];
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
-  int st = 0;
-  while (pos > 0 && !st) {
-    const Win w = win_load(bs, lo, pos);
+  const uint32_t sh = 64 - p;
+  while (pos >= K2_GROUP * LUT_MAX_BITS && count + K2_GROUP <= cap) {
+    const WinU w = winu_load(bs, base, pos);
     uint64_t acc = 0;
-    int got = 0;
+    uint32_t used = 0, bad = 0;
 #pragma unroll
-    for (int j = 0; j < K2_GROUP; j++) {
-      if (pos > 0 && !st) {
-        uint32_t idx = (uint32_t)(win_top(w, pos) >> (64 - p));
-        if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
-        const uint32_t e = lut[idx];
-        const int32_t nb = (int32_t)((e >> 8) & 0x7F);
-        if (e & LUT_ABSENT) st = nb <= pos ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
-        else if (nb > pos) st = ZD_E_NOT_ENOUGH_BITS;
-        else {
-          pos -= nb;
-          acc |= (uint64_t)(e & 0xFF) << (8 * got);
-          got++;
-        }
+    for (int h = 0; h < 2; h++) {
+      uint64_t t = winu_top(w, used);
+#pragma unroll
+      for (int j = 0; j < K2_GROUP / 2; j++) {
+        const uint32_t e = lut[(uint32_t)(t >> sh)];
+        const uint32_t nb = (e >> 8) & 0x7F;
+        bad |= e & LUT_ABSENT;
+        t <<= nb;
+        used += nb;
+        acc |= (uint64_t)(e & 0xFF) << (8 * (h * (K2_GROUP / 2) + j));
       }
     }
-    if (count + K2_GROUP <= cap && got == K2_GROUP) {
-      *(g_u64a1*)(out + count) = acc;
-    } else {
-      for (int j = 0; j < got; j++)
-        if (count + j < cap) out[count + j] = (uint8_t)(acc >> (8 * j));
+    if (bad) break;                            // redo this group with the exact checks
+    *(g_u64a1*)(out + count) = acc;
+    count += K2_GROUP;
+    pos -= (int32_t)used;
+  }
+  int st = 0;
+  while (pos > 0 && !st) {
+    const WinU w = winu_load(bs, base, pos);
+    uint32_t idx = (uint32_t)(winu_top(w, 0) >> sh);
+    if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
+    const uint32_t e = lut[idx];
+    const int32_t nb = (int32_t)((e >> 8) & 0x7F);
+    if (e & LUT_ABSENT) st = nb <= pos ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
+    else if (nb > pos) st = ZD_E_NOT_ENOUGH_BITS;
+    else {
+      pos -= nb;
+      if (count < cap) out[count] = (uint8_t)e;
+      count++;
     }
-    count += got;
   }
   *count_out = count;
   return st;
@@ -636,7 +621,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint32_t start = (uint32_t)k * seg;
     const uint32_t cap = k < m - 1 ? seg : (R > start ? R - start : 0);
     const uint8_t* blk = src + C.src;
-    const uintptr_t lo = (uintptr_t)blk & ~(uintptr_t)3;
+    const uintptr_t lo = (uintptr_t)src;
     uint32_t count;
     int st;
     if (use_lds)
@@ -680,10 +665,10 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     uint32_t count;
     const uint32_t at = redo_at[b][k];
     if (use_lds)
-      (void)huf_stream<const lds_u16*>(blk + off, C.stream_size[k], (uintptr_t)blk & ~(uintptr_t)3,
+      (void)huf_stream<const lds_u16*>(blk + off, C.stream_size[k], (uintptr_t)src,
                                        (const lds_u16*)lut[b], p, lits + C.lit_out + at, counts[b][k], &count);
     else
-      (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)blk & ~(uintptr_t)3, (g_u16*)g, p,
+      (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)src, (g_u16*)g, p,
                                lits + C.lit_out + at, counts[b][k], &count);
   }
 }
