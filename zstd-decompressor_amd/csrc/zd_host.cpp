@@ -325,6 +325,10 @@ struct zd_plan {
   bool profile = false;
   hipEvent_t ev[N_KERNELS + 1] = {};
   bool ev_made = false;
+  // second stream for the HBM-table K3 kernel (created on first launch)
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  float k3_lds_frac = K3_LDS_FRAC_DEFAULT;
   bool launched = false;
   // context API hook: comp 0 is a prebuilt "previous block" carrying tables
   bool has_prebuilt = false;
@@ -615,6 +619,9 @@ void zd_plan_destroy(zd_plan* P) {
   if (P->d_ws) (void)hipFree(P->d_ws);
   if (P->d_staging) (void)hipFree(P->d_staging);
   if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
+  if (P->fork) (void)hipEventDestroy(P->fork);
+  if (P->join) (void)hipEventDestroy(P->join);
+  if (P->aux) (void)hipStreamDestroy(P->aux);
   delete P;
 }
 
@@ -662,6 +669,16 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_frames = (uint32_t)P->fdesc.size();
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
+  if (const char* f = getenv("ZD_K3_LDS_FRAC")) P->k3_lds_frac = (float)atof(f);   // experiments
+  if (P->k3_lds_frac < 1.0f && !P->aux) {
+    HIPCHK(hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&P->fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&P->join, hipEventDisableTiming));
+  }
+  a.aux = P->aux;
+  a.fork = P->fork;
+  a.join = P->join;
+  a.k3_lds_frac = P->k3_lds_frac;
   HIPCHK(launch_pipeline(a));
   P->launched = true;
   return ZD_OK;

@@ -758,6 +758,50 @@ __device__ int seq_block(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP
   return st;
 }
 
+// Block epilogue shared by both K3 kernels.
+__device__ inline void k3_finish(const CompBlock& C, uint32_t ci, CompState* cstate, FrameState* fstate, int st,
+                                 const uint32_t rep[3]) {
+  if (st) {
+    key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
+    cstate[ci].stop = 1;
+  } else {
+    cstate[ci].rep_out[0] = rep[0];
+    cstate[ci].rep_out[1] = rep[1];
+    cstate[ci].rep_out[2] = rep[2];
+  }
+}
+
+// K3 with the tables in HBM (L2-resident), no LDS: runs beside zd_k_sequences
+// on a second stream so the SIMDs the LDS-bound kernel leaves idle decode
+// more blocks (the split is LaunchArgs::k3_lds_blocks).
+constexpr int K3G_LANES = 64;
+__global__ __launch_bounds__(K3G_LANES) void zd_k_sequences_hbm(const uint8_t* __restrict__ src,
+                                                                const CompBlock* __restrict__ comp,
+                                                                CompState* cstate, FrameState* fstate,
+                                                                const uint32_t* __restrict__ list, uint32_t n_list,
+                                                                const uint16_t* __restrict__ fses,
+                                                                uint64_t* __restrict__ seqs) {
+  const uint32_t li = blockIdx.x * K3G_LANES + threadIdx.x;
+  if (li >= n_list) return;
+  const uint32_t ci = list[li];
+  const CompBlock C = comp[ci];
+  const uint64_t key0 = fstate[C.frame].key;
+  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
+  int al[3];
+  const uint16_t* g[3];
+  for (int k = 0; k < 3; k++) {
+    const uint32_t s = (uint32_t)C.tab_src[k];
+    al[k] = cstate[s].al[k];
+    g[k] = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+  }
+  const CompState cs = cstate[ci];
+  uint32_t rep[3];
+  rep_init(rep);
+  const int st = seq_block<g_u16*>(src + C.src + cs.bs_off, cs.bs_size, (uintptr_t)src, (g_u16*)g[0], (g_u16*)g[2],
+                                   (g_u16*)g[1], al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
+  k3_finish(C, ci, cstate, fstate, st, rep);
+}
+
 __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __restrict__ src,
                                                            const CompBlock* __restrict__ comp, CompState* cstate,
                                                            FrameState* fstate, const uint32_t* __restrict__ list,
@@ -817,14 +861,7 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
   else
     st = seq_block<g_u16*>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2],
                            (g_u16*)g[1], al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
-  if (st) {
-    key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
-    cstate[ci].stop = 1;
-  } else {
-    cstate[ci].rep_out[0] = rep[0];
-    cstate[ci].rep_out[1] = rep[1];
-    cstate[ci].rep_out[2] = rep[2];
-  }
+  k3_finish(C, ci, cstate, fstate, st, rep);
 }
 
 // ---------------------------------------------------------------------------
@@ -920,23 +957,20 @@ __device__ void k4_flush(K4& X, bool final) {
   }
 }
 
-// Slides the window so that at least K4_B - 16 bytes are free (keeps K4_W of history).
+// Slides the window so that at least K4_B - 16 bytes are free (keeps K4_W of
+// history).  An ascending chunked copy: each 1 KiB step reads all its chunks
+// before writing any, and later steps read above everything written so far.
 __device__ void k4_room(K4& X) {
   if (X.space() >= K4_B) return;
   const int64_t nh = ((X.oabs + X.pos - K4_W) & ~(intptr_t)15) - X.oabs;   // <= fl: pos - fl < 16
   const int64_t n = X.pos - nh;                // <= K4_W + 15 bytes move down by nh - hs
-  constexpr int PER = (K4_W + 16 + 1023) / 1024;
-  u32x4 keep[PER];
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const int64_t x = 16 * X.lane + 1024 * r;
-    if (x < n) keep[r] = lds16(X.at(nh + x));
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const int64_t x = 16 * X.lane + 1024 * r;
-    if (x < n) *(l_u32x4a1*)(X.buf + x) = keep[r];
+  const l_u8* from = X.at(nh);
+  for (int64_t x = 16 * X.lane; x - 16 * X.lane < n; x += 1024) {
+    u32x4 v;
+    if (x < n) v = lds16(from + x);
+    __builtin_amdgcn_wave_barrier();
+    if (x < n) *(l_u32x4a1*)(X.buf + x) = v;
+    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
   X.hs = nh;
@@ -1219,9 +1253,30 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
-  if (a.n_seq)
-    hipLaunchKernelGGL(zd_k_sequences, dim3((a.n_seq + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
-                       cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses, seqs);
+  if (a.n_seq) {
+    // blocks [0, n_lds) on the LDS kernel, the rest on the HBM-table kernel
+    // on the aux stream, concurrently
+    const uint32_t* list = (const uint32_t*)(ws + W.list_seq);
+    uint32_t n_lds = a.n_seq;
+    if (a.aux && a.k3_lds_frac < 1.0f) {
+      n_lds = (uint32_t)((double)a.n_seq * a.k3_lds_frac) / K3_LANES * K3_LANES;
+      if (n_lds > a.n_seq) n_lds = a.n_seq;
+    }
+    const uint32_t n_hbm = a.n_seq - n_lds;
+    if (n_hbm) {
+      if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
+      hipLaunchKernelGGL(zd_k_sequences_hbm, dim3((n_hbm + K3G_LANES - 1) / K3G_LANES), dim3(K3G_LANES), 0, a.aux,
+                         a.src, comp, cstate, fstate, list + n_lds, n_hbm, (const uint16_t*)fses, seqs);
+    }
+    if (n_lds)
+      hipLaunchKernelGGL(zd_k_sequences, dim3((n_lds + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
+                         cstate, fstate, list, n_lds, (const uint16_t*)fses, seqs);
+    if (n_hbm) {
+      if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
+    }
+  }
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   if (a.n_frames)
     hipLaunchKernelGGL(zd_k_execute, dim3(a.n_frames), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
