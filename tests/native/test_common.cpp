@@ -1,7 +1,8 @@
 // Host unit test of the arithmetic shared by the kernels and the host
 // (zstd-decompressor_amd/csrc/zd_common.h): sequence-code baselines, the
-// 16-bit FSE entry, and the symbolic repeat-offset codes against a direct
-// restatement of DecodingContext::decode_offset (decoding_context.rs:50-75).
+// 16-bit FSE entry, K3's chain entries, direct sequence records, and K4's
+// batch walk of the repeat offsets against a direct restatement of
+// DecodingContext::decode_offset (decoding_context.rs:50-75).
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -50,32 +51,81 @@ int main() {
       CHECK(nb == (uint32_t)(al - hb) && base == (ns << (al - hb)) - T && fse_sym(e) == 5, "fse al %d ns %u", al, ns);
     }
   }
-  // packed record round trip
+  // K3 chain entries: nextState, extra bits of the code, code-max flag
+  for (int k = 0; k < 3; k++) {
+    for (uint32_t c = 0; c < 64; c++) {
+      for (uint32_t ns = 1; ns < 1024; ns += 37) {
+        uint32_t e = k3_entry(fse_entry(c, ns), k);
+        uint32_t bits = k == 0 ? (c < 36 ? LL_BITS[c] : 0) : (k == 2 ? (c < 53 ? ML_BITS[c] : 0) : c);
+        bool bad = k == 0 ? c > 35 : (k == 2 ? c > 52 : c > 31);
+        CHECK((e & 1023) == ns, "k3 ns");
+        CHECK(((e & K3_BAD) != 0) == bad, "k3 bad k=%d c=%u", k, c);
+        if (!bad) CHECK(((e >> 10) & 31) == bits, "k3 bits k=%d c=%u", k, c);
+      }
+    }
+  }
+  // direct records round trip (offset values past DIRECT_GIANT saturate)
   std::mt19937_64 g(7);
   for (int i = 0; i < 100000; i++) {
-    uint32_t ll = g() % 131072, ml = g() % 131075, oc = g() % (1u << 29);
-    uint64_t s = seq_pack(ll, ml, oc);
-    CHECK(seq_ll(s) == ll && seq_ml(s) == ml && seq_off(s) == oc, "pack");
+    uint32_t ll = g() % 131072, ml = g() % 131075, ov = (uint32_t)g();
+    uint64_t s = seq_pack(ll, ml, ov);
+    CHECK(seq_ll(s) == ll && seq_ml(s) == ml && seq_off(s) == (ov > DIRECT_GIANT ? DIRECT_GIANT : ov), "pack");
   }
-  // symbolic repeat offsets == direct decode_offset, per block, from random
-  // incoming states, including rep0-1 chains, zeros and underflows
+  // K4's batch walk of decode_offset (zd_kernels.hip zd_k_execute): fresh
+  // offsets direct, repeat codes walked in order from the state the fresh
+  // lanes before them pushed; the state after lane k - 1 the same way.
   for (int trial = 0; trial < 20000; trial++) {
-    uint64_t in[3];
-    for (int k = 0; k < 3; k++) in[k] = (g() % 4 == 0) ? g() % 3 : 1 + g() % 100000;
-    uint64_t o[3] = {in[0], in[1], in[2]};
-    uint32_t r[3]; rep_init(r);
-    int n = 1 + g() % 40;
+    uint64_t o[3];
+    for (int k = 0; k < 3; k++) o[k] = (g() % 4 == 0) ? g() % 3 : 1 + g() % 100000;
+    uint64_t rep[3] = {o[0], o[1], o[2]};
+    int n = 1 + g() % 64, kexec = 1 + g() % n;
+    uint64_t ofv[64], ll[64], val[64];
     for (int i = 0; i < n; i++) {
-      uint64_t ofv; uint32_t ll = (g() % 3 == 0) ? 0 : 1 + g() % 50;
       uint64_t pick = g() % 10;
-      ofv = pick < 7 ? 1 + g() % 3 : (pick < 9 ? 4 + g() % 5000 : (g() % 50 == 0 ? 0 : (1ull << 28) + 3 + g() % 1000));
-      uint64_t want = 0; int wst = ref_decode(o, ofv, ll, &want);
-      uint32_t code = rep_step(r, (uint32_t)ofv, ll);
-      uint64_t got = 0; int gst = off_resolve(code, in, &got);
-      if (wst) { CHECK(gst == wst, "trial %d seq %d: status %d vs %d", trial, i, gst, wst); break; }
-      CHECK(gst == 0, "trial %d seq %d: unexpected status %d", trial, i, gst);
-      if (want >= (1ull << 28) - (1ull << 24)) CHECK(got >= (1ull << 27), "giant offset %llu -> %llu", (unsigned long long)want, (unsigned long long)got);
-      else CHECK(got == want, "trial %d seq %d: off %llu vs %llu", trial, i, (unsigned long long)got, (unsigned long long)want);
+      ll[i] = (g() % 3 == 0) ? 0 : 1 + g() % 50;
+      ofv[i] = pick < (trial % 2 ? 2 : 7) ? 1 + g() % 3 : (pick < 9 ? 4 + g() % 5000 : (g() % 50 == 0 ? 0 : 4 + g() % 7));
+      val[i] = ofv[i] - 3;
+    }
+    auto push = [&](int cnt, int end, const uint64_t r[3], uint64_t a[3]) {
+      a[0] = r[0]; a[1] = r[1]; a[2] = r[2];
+      if (cnt >= 1) { a[0] = val[end - 1]; a[1] = r[0]; a[2] = r[1]; }
+      if (cnt >= 2) { a[1] = val[end - 2]; a[2] = r[0]; }
+      if (cnt >= 3) a[2] = val[end - 3];
+    };
+    uint64_t r[3] = {rep[0], rep[1], rep[2]};
+    uint64_t off[64];
+    int err[64] = {0};
+    int prev = -1, stop = -1;
+    for (int i = 0; i < kexec; i++) {
+      off[i] = val[i];
+      if (ofv[i] > 3) continue;
+      uint64_t a[3];
+      push(i - prev - 1, i, r, a);
+      int e = 0; uint64_t v = 0;
+      if (ofv[i] == 0) e = -41;
+      else {
+        uint32_t idx = (uint32_t)ofv[i] - (ll[i] != 0 ? 1 : 0);
+        if (idx == 0) v = a[0];
+        else if (idx == 1) { v = a[1]; a[1] = a[0]; a[0] = v; }
+        else if (idx == 2) { v = a[2]; a[2] = a[1]; a[1] = a[0]; a[0] = v; }
+        else if (a[0] == 0) e = -90;
+        else { v = a[0] - 1; a[2] = a[1]; a[1] = a[0]; a[0] = v; }
+      }
+      off[i] = v; err[i] = e;
+      r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+      prev = i;
+      if (e) { stop = i; break; }
+    }
+    uint64_t after[3];
+    push(kexec - 1 - prev, kexec, r, after);
+    // direct restatement
+    uint64_t want;
+    for (int i = 0; i < kexec; i++) {
+      int wst = ref_decode(o, ofv[i], ll[i], &want);
+      if (wst) { CHECK(stop == i && err[i] == wst, "trial %d seq %d: status %d vs %d", trial, i, err[i], wst); break; }
+      CHECK(off[i] == want, "trial %d seq %d: off %llu vs %llu", trial, i, (unsigned long long)off[i], (unsigned long long)want);
+      if (i == kexec - 1)
+        CHECK(after[0] == o[0] && after[1] == o[1] && after[2] == o[2], "trial %d: state after the batch", trial);
     }
   }
   if (fails) { printf("%d failures\n", fails); return 1; }

@@ -1,6 +1,7 @@
 """Host unit test of the arithmetic the kernels share with the host
 (zd_common.h): sequence-code baselines, 16-bit FSE entries, packed sequence
-records and symbolic repeat offsets vs decode_offset (decoding_context.rs:50-75).
+records, K3 chain entries and K4's repeat-offset batch walk vs decode_offset
+(decoding_context.rs:50-75).
 Compiled with g++ from tests/native/test_common.cpp; no GPU needed."""
 import os
 import subprocess

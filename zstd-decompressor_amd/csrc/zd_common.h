@@ -67,79 +67,42 @@ ZD_HD inline void ml_code(uint32_t c, uint32_t* base, uint32_t* bits) {
   *base = c < 32 ? c + 3 : (c < 43 ? mbase : (1u << hi) + 3);
 }
 
-// ---------------------------------------------------------------------------
-// Decoded sequence record (K3 -> K4), 8 bytes:
-//   bits 0-16 literals_length (<= 131071), 17-34 match_length (<= 131074),
-//   35-63 offset code.
-// The offset code is DecodingContext::decode_offset (decoding_context.rs:
-// 50-75) evaluated per block against a *symbolic* incoming repeat state, so
-// blocks decode in parallel; K4 resolves it against the real state:
-//   v <  OFF_SYM                    concrete offset v
-//   OFF_SYM + (slot << 24) + d      incoming rep[slot] - d (d decrements of
-//                                   the `3, ll == 0` rule; underflow when
-//                                   rep[slot] < d: the reference panics)
-//   OFF_GIANT                       an offset >= 2^28: past any frame the GPU
-//                                   path accepts (ImpossibleValue)
-//   OFF_NULL                        offset_value 0 (NullOffsetError)
-//   OFF_UNDERFLOW                   usize underflow of rep0 - 1 (ZD_E_REF_PANIC)
-// ---------------------------------------------------------------------------
-constexpr uint32_t OFF_SYM = 1u << 28;
-constexpr uint32_t OFF_GIANT = (1u << 29) - 3;
-constexpr uint32_t OFF_NULL = (1u << 29) - 2;
-constexpr uint32_t OFF_UNDERFLOW = (1u << 29) - 1;
-constexpr uint64_t MAX_FRAME_OUT = 1ull << 27;   // frames the GPU path decodes (OFF_GIANT stays impossible)
+// K3's chain-format table entry (16 bits), re-encoded from a sym entry of
+// table k (0 LL, 1 OF, 2 ML) when K3 loads it into LDS: nextState (10 bits)
+// | extra-bit count of the symbol's code << 10 (5 bits) | K3_BAD for a code
+// above the maximum (LL 35, OF 31, ML 52: decoders/sequence.rs:95-97).
+constexpr uint32_t K3_BAD = 1u << 15;
+ZD_HD inline uint32_t k3_entry(uint32_t e, int k) {
+  const uint32_t c = e & 63, ns = (e >> 6) & 1023;
+  uint32_t base, eb, bad;
+  if (k == 0) { ll_code(c, &base, &eb); bad = c > 35; }
+  else if (k == 2) { ml_code(c, &base, &eb); bad = c > 52; }
+  else { eb = c; bad = c > 31; }
+  return ns | ((eb & 31) << 10) | (bad ? K3_BAD : 0u);
+}
 
-ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t offc) {
-  return (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)offc << 35);
+// ---------------------------------------------------------------------------
+// Sequence records (K3 -> K4), 8 bytes each:
+//   from K3 (FSE chain): low 32 bits = bit position of the sequence's extra
+//     bits (their top, before OF/ML/LL are read), high 32 bits = LL | ML << 10
+//     | OF << 20 states; K4 decodes the values (decoders/sequence.rs:41-55).
+//   direct (zd_execute_sequences, CompBlock::seq_direct): bits 0-16
+//     literals_length, 17-34 match_length, 35-63 offset_value, where
+//     DIRECT_GIANT stands for any offset_value >= 2^29 - 1 (an offset past
+//     every frame the GPU path accepts: ImpossibleValue when used).
+// Repeat offsets (decoding_context.rs:50-75) are resolved by K4 in frame
+// order with concrete values.
+// ---------------------------------------------------------------------------
+constexpr uint32_t DIRECT_GIANT = (1u << 29) - 1;
+constexpr uint64_t MAX_FRAME_OUT = 1ull << 27;   // frames with sequences the GPU path decodes
+constexpr uint64_t OFF_HUGE = ~0ull >> 1;        // a giant offset (never <= a decoded length)
+
+ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t ofv) {
+  return (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)(ofv > DIRECT_GIANT ? DIRECT_GIANT : ofv) << 35);
 }
 ZD_HD inline uint32_t seq_ll(uint64_t s) { return (uint32_t)(s & 0x1FFFF); }
 ZD_HD inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >> 17) & 0x3FFFF); }
 ZD_HD inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 35); }
-
-ZD_HD inline void rep_init(uint32_t r[3]) { r[0] = OFF_SYM; r[1] = OFF_SYM | (1u << 24); r[2] = OFF_SYM | (2u << 24); }
-ZD_HD inline uint32_t rep_dec1(uint32_t v) {
-  // giant stays giant; after an underflow the reference stopped; a symbolic
-  // value counts one more decrement; 0 underflows.  Written as a chain of
-  // selects (no divergent branches in the per-lane decoder).
-  uint32_t t = v >= OFF_SYM ? v + 1 : v - 1;
-  t = v == 0 ? OFF_UNDERFLOW : t;
-  return v >= OFF_GIANT ? v : t;
-}
-// decode_offset (decoding_context.rs:50-75) on codes; returns the offset code.
-// idx = the repeat slot an offset_value <= 3 names (RFC 8878 3.1.1.5), 3
-// being `rep0 - 1`.
-ZD_HD inline uint32_t rep_step(uint32_t r[3], uint32_t ofv, uint32_t ll) {
-  const uint32_t r0 = r[0], r1 = r[1], r2 = r[2];
-  const bool fresh = ofv > 3;
-  const uint32_t idx = ofv - (ll != 0 ? 1u : 0u);
-  uint32_t rep = idx == 0 ? r0 : r1;
-  rep = idx >= 2 ? r2 : rep;
-  rep = idx == 3 ? rep_dec1(r0) : rep;
-  const uint32_t v = ofv - 3;
-  const uint32_t n0 = fresh ? (v >= OFF_SYM ? OFF_GIANT : v) : rep;
-  const uint32_t n1 = (!fresh && idx == 0) ? r1 : r0;
-  const uint32_t n2 = (!fresh && idx <= 1) ? r2 : r1;
-  const bool null = ofv == 0;
-  r[0] = null ? r0 : n0;
-  r[1] = null ? r1 : n1;
-  r[2] = null ? r2 : n2;
-  return null ? OFF_NULL : n0;
-}
-// Resolves an offset code against the block's incoming repeat offsets.
-// Returns 0 and *off, or the reference's error for this decode_offset.
-constexpr uint64_t OFF_HUGE = ~0ull >> 1;
-ZD_HD inline int off_resolve(uint32_t v, const uint64_t in[3], uint64_t* off) {
-  if (v < OFF_SYM) { *off = v; return 0; }
-  if (v < OFF_GIANT) {
-    uint32_t slot = (v - OFF_SYM) >> 24, d = (v - OFF_SYM) & 0xFFFFFF;
-    uint64_t b = slot == 0 ? in[0] : (slot == 1 ? in[1] : in[2]);
-    if (b < d) return -90;                  // ZD_E_REF_PANIC (usize underflow)
-    *off = b - d;
-    return 0;
-  }
-  if (v == OFF_GIANT) { *off = OFF_HUGE; return 0; }
-  return v == OFF_NULL ? -41 /* ZD_E_NULL_OFFSET */ : -90 /* ZD_E_REF_PANIC */;
-}
 
 // ---------------------------------------------------------------------------
 // Error keys.  The reference parses every block of a frame (tables included)
@@ -193,6 +156,7 @@ struct CompBlock {
   uint8_t modes[3];        // raw LL/OF/ML modes of the mode byte
   uint8_t host_stage;      // GPU parse runs only parse stages < host_stage
   uint8_t prebuilt;        // 1: tables already present in the slots (context API); skip
+  uint8_t seq_direct;      // 1: the sequence records are direct {ll, ml, offset_value} (zd_common.h)
 };
 
 // Results per compressed block (device).
@@ -203,8 +167,6 @@ struct CompState {
   uint32_t stop;           // nonzero: literals/sequences stage failed or is out of domain
   uint8_t al[3];           // accuracy log of the LL/OF/ML table in this block's FSE slot
   uint8_t huf_bits;        // maxBits of this block's LUT
-  uint32_t rep_out[3];     // repeat-offset codes after the block (symbolic in the incoming ones)
-  uint32_t _pad;
 };
 
 // Blocks of frames in order (all types).

@@ -325,10 +325,6 @@ struct zd_plan {
   bool profile = false;
   hipEvent_t ev[N_KERNELS + 1] = {};
   bool ev_made = false;
-  // second stream for the HBM-table K3 kernel (created on first launch)
-  hipStream_t aux = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  float k3_lds_frac = K3_LDS_FRAC_DEFAULT;
   bool launched = false;
   // context API hook: comp 0 is a prebuilt "previous block" carrying tables
   bool has_prebuilt = false;
@@ -342,7 +338,7 @@ uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // Treeless/Repeat resolution (context API), -1 when absent.
 int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
                const uint64_t rep0[3], uint64_t fixed_cap) {
-  uint64_t lits = 0, nseq_total = 0, out_off = 0;
+  uint64_t lits = 0, nseq_total = 0, nrec = 0, out_off = 0;
   uint32_t lut_slots = 0, fse_slots = 0;
   bool exact = true;
   P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear();
@@ -409,8 +405,9 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
           cb.lit_out = lits;
           lits += align_up((uint64_t)cb.lit_regen + 16, 16);
         }
-        cb.seq_out = nseq_total;
+        cb.seq_out = nrec;
         nseq_total += cb.nseq;
+        nrec += cb.nseq + (cb.nseq ? 1 : 0);     // K3 writes one spare record past the block's last
         seqs_in_frame |= cb.nseq > 0;
         P->comps.push_back(cb);
         br.comp = (int32_t)ci;
@@ -467,7 +464,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
   W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
   W.lits = carve(lits + 64);
-  W.seqs = carve(8 * nseq_total + 64);
+  W.seqs = carve(8 * nrec + 64);
   W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
   W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint32_t>(fse_slots, 1));
   W.total = o;
@@ -619,9 +616,6 @@ void zd_plan_destroy(zd_plan* P) {
   if (P->d_ws) (void)hipFree(P->d_ws);
   if (P->d_staging) (void)hipFree(P->d_staging);
   if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
-  if (P->fork) (void)hipEventDestroy(P->fork);
-  if (P->join) (void)hipEventDestroy(P->join);
-  if (P->aux) (void)hipStreamDestroy(P->aux);
   delete P;
 }
 
@@ -669,16 +663,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_frames = (uint32_t)P->fdesc.size();
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
-  if (const char* f = getenv("ZD_K3_LDS_FRAC")) P->k3_lds_frac = (float)atof(f);   // experiments
-  if (P->k3_lds_frac < 1.0f && !P->aux) {
-    HIPCHK(hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&P->fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&P->join, hipEventDisableTiming));
-  }
-  a.aux = P->aux;
-  a.fork = P->fork;
-  a.join = P->join;
-  a.k3_lds_frac = P->k3_lds_frac;
+  if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
   HIPCHK(launch_pipeline(a));
   P->launched = true;
   return ZD_OK;
@@ -1028,7 +1013,7 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   memset(&hb, 0, sizeof hb);
   hb.type = 2; hb.size = (uint32_t)nlits; hb.src = 0; hb.last = 1;
   hb.cb.lit_type = LIT_RAW; hb.cb.lit_regen = (uint32_t)nlits; hb.cb.lit_data = 0;
-  hb.cb.nseq = (uint32_t)nseq; hb.cb.host_stage = PS_ALL;
+  hb.cb.nseq = (uint32_t)nseq; hb.cb.host_stage = PS_ALL; hb.cb.seq_direct = 1;
   hb.cb.modes[0] = hb.cb.modes[1] = hb.cb.modes[2] = M_RLE;
   hf.blocks.push_back(hb);
   P.frames.push_back(hf);
@@ -1051,16 +1036,16 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   if (r) return fin(r);
   if (hipMalloc(&d_src, nlits + ZD_SRC_PADDING) != hipSuccess) return fin(ZD_E_HIP);
   if (nlits && hipMemcpy(d_src, lits, nlits, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
-  // the caller's triples in K3's record format (offset codes symbolic in
-  // the context's repeat offsets; zd_common.h)
+  // the caller's triples as direct records (zd_common.h); offsets are
+  // exact below DIRECT_GIANT, which stays past every decoded length here
   CompState cs{};
   cs.lit_count = (uint32_t)nlits;
-  rep_init(cs.rep_out);
   if (nseq) {
+    if (need >= DIRECT_GIANT - 3) return fin(ZD_E_OUT_OF_DOMAIN);
     std::vector<uint64_t> rec(nseq);
     for (size_t i = 0; i < nseq; i++) {
       if (ll[i] > 0x1FFFF || ml[i] > 0x3FFFF) return fin(ZD_E_OUT_OF_DOMAIN);
-      rec[i] = seq_pack(ll[i], ml[i], rep_step(cs.rep_out, ofv[i], ll[i]));
+      rec[i] = seq_pack(ll[i], ml[i], ofv[i]);
     }
     if (hipMemcpy(P.d_ws + P.W.seqs, rec.data(), nseq * 8, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
   }

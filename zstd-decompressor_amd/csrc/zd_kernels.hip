@@ -674,139 +674,260 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
 }
 
 // ---------------------------------------------------------------------------
-// K3: sequences (sequences.rs:191-237, decoders/sequence.rs:30-93), one block
-// per LANE.  The FSE chain of a block is strictly serial, so parallelism comes
-// from blocks: each lane runs one block's three-state machine with its tables
-// in LDS (16-bit entries, LL 512 | ML 512 | OF 256 per lane), the bitstream
-// read through a 128-bit register window that is reloaded one step ahead
-// (the next step's exact bit position is known once this step's table
-// entries are read, so the reload's latency hides behind the rest of the
-// step).  Offsets leave as repeat-offset codes (zd_common.h), symbolic in the
-// block's incoming repeat offsets, so blocks of one frame decode in parallel.
-// A lane whose OF table is deeper than 256 states (AL 9; never produced by
-// zstd, whose offset tables are AL <= 8) makes its workgroup read tables from
-// HBM instead.
+// K3: sequences (sequences.rs:191-237, decoders/sequence.rs:30-93) — the FSE
+// state chain only, one block per LANE.  The chain of a block is strictly
+// serial (each state update reads bits whose position depends on the
+// previous step), so K3 does the least per step that the chain needs: three
+// LDS table lookups, the bit position, the three state updates.  It records
+// per sequence {bit position before its extra bits, LL/ML/OF states}; the
+// values (codes -> baselines, extra bits, repeat offsets) are independent
+// per sequence once those are known and are decoded in parallel by K4.
+//
+// Tables live in LDS, re-encoded on load for the chain (zd_common.h
+// k3_entry: nextState | extra-bit count of the symbol << 10 | code-max flag),
+// LL 512 | ML 512 | OF 256 entries per lane.  A lane whose OF table is deeper
+// than 256 states (AL 9; zstd's offset tables are AL <= 8) makes its
+// workgroup use HBM tables in the sym format instead (slow path).
 // ---------------------------------------------------------------------------
 #ifndef ZD_K3_LANES
-#define ZD_K3_LANES 32
+#define ZD_K3_LANES 16
 #endif
 constexpr int K3_LANES = ZD_K3_LANES;
+#ifdef ZD_K3_W1
+#define K3_CHAIN seq_chain       // window one step ahead (reference variant for experiments)
+#else
+#define K3_CHAIN seq_chain2      // window two steps ahead (default: 23.8 -> 18.3 ms on C4)
+#endif
 constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
 static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
 
-// Runs one block's sequences; TP is an LDS (lds_u16*) or HBM (g_u16*) table
-// pointer.  Returns 0 or the reference's error.
-template <typename TP>
-__device__ int seq_block(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
-                         int alo, int alm, uint32_t n, uint64_t* __restrict__ out, uint32_t rep[3]) {
+// 128-bit window of a backward bitstream: bits [wb, wb + 128) of the stream
+// (bit 0 = LSB of byte 0), loaded unaligned as the 16 bytes ending at the
+// byte that holds bit pos - 1, clamped at the input base.
+typedef uint32_t u32x4ua __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4ua g_u32x4ua;
+struct Win4 {
+  uint32_t w0, w1, w2, w3;
+  int32_t wb;
+};
+// m = base - s (<= 0): the lowest byte offset the window may start at.
+__device__ inline Win4 win4_load(const uint8_t* s, int32_t m, int32_t pos) {
+  const int32_t tb = (pos + 7) >> 3;
+  const int32_t o = max(tb - 16, m);
+  const u32x4ua v = *(g_u32x4ua*)(s + o);
+  Win4 w;
+  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w;
+  w.wb = o * 8;
+  return w;
+}
+// The S bits [p - S, p) of the stream, S <= 32, MSB-first value; requires
+// wb <= p - S and p <= wb + 128 (else garbage, never a memory access).
+__device__ inline uint32_t win4_bits(const Win4& w, int32_t p, uint32_t S) {
+  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
+  const uint32_t k = y >> 5;
+  uint32_t lo = k == 0 ? w.w0 : w.w1;
+  uint32_t hi = k == 0 ? w.w1 : w.w2;
+  lo = k >= 2 ? w.w2 : lo;
+  hi = k >= 2 ? w.w3 : hi;
+  lo = k >= 3 ? w.w3 : lo;
+  hi = k >= 3 ? 0u : hi;
+  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
+}
+
+__device__ inline void k3_store(uint64_t* p, uint32_t pos, uint32_t states) {
+  const uint64_t v = (uint64_t)pos | ((uint64_t)states << 32);
+#ifdef ZD_K3_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+// One block's FSE chain.  TP: LDS (k3 entries) or HBM (sym entries, K3_SYM).
+// Returns 0 or the reference's error (the block then never executes).
+template <typename TP, bool K3_SYM>
+__device__ int seq_chain(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
+                         int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
   // BackwardBitParser::new (parsing.rs:200-220)
   if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
   const uint8_t lastb = bs[bs_size - 1];
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
-  WinU w = winu_load(bs, base, pos);
-  // SequenceDecoder::initialize: LL, OF, ML (sequence.rs:59-65)
-  if (all + alo + alm > pos) return ZD_E_NOT_ENOUGH_BITS;
-  uint64_t t0 = winu_top(w, 0);
-  uint32_t sLL = take_top(t0, all), sOF = take_top(t0, alo), sML = take_top(t0, alm);
-  pos -= all + alo + alm;
-  w = winu_load(bs, base, pos);
-  // consume the first window here, so the loop head's wait covers only the
-  // latch's load (vmcnt(1): the step's store may stay in flight)
-  asm volatile("" : "+v"(w.w0), "+v"(w.w1));
-  // nb = AL - highbit(ns) = clz(ns) + (AL - 31)
-  const int aL = all - 31, aM = alm - 31, aO = alo - 31;
+  // SequenceDecoder::initialize: LL, OF, ML, each take(al) from the top (sequence.rs:59-65)
+  const int32_t A = all + alo + alm;
+  if (A > pos) return ZD_E_NOT_ENOUGH_BITS;
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-16);
+  Win4 w = win4_load(bs, m, pos);
+  const uint32_t v0 = win4_bits(w, pos, (uint32_t)A);
+  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
+  pos -= A;
+  w = win4_load(bs, m, pos);
+  // nb = AL - highbit(ns) = clz(ns) + (AL - 31); baseline = (ns << nb) - T
+  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
   const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
-  // One exit at the bottom and no other branches: the body is straight-line,
-  // so the next window's load lands directly in the window registers (no
-  // copy that would wait on it).  A failing step still runs to the bottom:
-  // states stay inside their tables (valid FSE tables map every state and
-  // bit pattern to a state < T) and window loads clamp, so nothing strays.
+  // Record i is stored at the end of step i - 1, after the load of step i's
+  // window: vmcnt drains in issue order, so each step waits for its window
+  // and never for the record store just before it.  The block's records
+  // have one spare slot past the last (host: seq_out), so the final step
+  // stores without a branch.
+  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
   int st = 0;
   for (uint32_t i = 0;; i++) {
-    const uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
-    const uint32_t llc = eLL & 63, ofc = eOF & 63, mlc = eML & 63;
-    const bool codemax = llc > 35 || mlc > 52 || ofc > 31;
-    uint32_t llbase, llb, mlbase, mlb;
-    ll_code(llc, &llbase, &llb);
-    ml_code(mlc, &mlbase, &mlb);
-    const uint32_t nsL = eLL >> 6, nsM = eML >> 6, nsO = eOF >> 6;
-    const uint32_t nbL = __clz(nsL) + aL, nbM = __clz(nsM) + aM, nbO = __clz(nsO) + aO;
-    const uint32_t E = (ofc & 31) + mlb + llb;
+    uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
+    if (K3_SYM) {
+      eLL = k3_entry(eLL, 0);
+      eOF = k3_entry(eOF, 1);
+      eML = k3_entry(eML, 2);
+    }
+    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
+    // ns >= 1 in every table K1 builds: clz without the zero case
+    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
+    // update_symbol_value (sequence.rs:41-55) reads OF, ML, LL extra bits
+    const uint32_t E = ((eLL >> 10) & 31) + ((eML >> 10) & 31) + ((eOF >> 10) & 31);
+    const bool codemax = ((eLL | eML | eOF) & K3_BAD) != 0;
     const bool last = i + 1 == n;
     const uint32_t S = last ? 0 : nbL + nbM + nbO;
     st = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : ((int32_t)(E + S) > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
-    // every use of this step's window precedes the next window's load, and
-    // the load precedes this step's store: the next step waits on the load only
-    uint64_t t = winu_top(w, 0);
-    uint64_t t2 = winu_top(w, E);
-    pos -= (int32_t)(E + S);
-    asm volatile("" : "+v"(t), "+v"(t2)::"memory");   // the window's reads stay above its reload
-    w = winu_load(bs, base, pos);
-    // update_symbol_value (sequence.rs:41-55): OF, ML, LL extra bits
-    const uint32_t ob = take_top(t, ofc & 31), mb = take_top(t, mlb), lb = take_top(t, llb);
-    const uint32_t ofv = (1u << (ofc & 31)) + ob, ml = mlbase + mb, ll = llbase + lb;
-    out[i] = seq_pack(ll, ml, rep_step(rep, ofv, ll));
-    // update_bits: LL, ML, OF (sequence.rs:80-88)
-    const uint32_t vL = take_top(t2, nbL), vM = take_top(t2, nbM), vO = take_top(t2, nbO);
-    sLL = ((nsL << nbL) - TL) + vL;
-    sML = ((nsM << nbM) - TM) + vM;
-    sOF = ((nsO << nbO) - TO) + vO;
+    // update_bits: LL, ML, OF (sequence.rs:80-88), below the extra bits
+    const int32_t p2 = pos - (int32_t)E;
+    const uint32_t v = win4_bits(w, p2, S);
+    pos = p2 - (int32_t)S;
+#if defined(ZD_EXP_NOLOAD)
+    w.wb = pos - 100;                                 // experiment: stale window bits, no load
+#else
+    w = win4_load(bs, m, pos);
+#endif
+    const uint32_t vO = __builtin_amdgcn_ubfe(v, 0, nbO), vM = __builtin_amdgcn_ubfe(v, nbO, nbM);
+    const uint32_t vL = v >> (nbO + nbM);
+    sLL = (nsL << nbL) + vL - TL;
+    sML = (nsM << nbM) + vM - TM;
+    sOF = (nsO << nbO) + vO - TO;
+    asm volatile("" ::: "memory");                    // the store stays below the load
+#ifndef ZD_EXP_NOSTORE
+    k3_store(out + i + 1, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+#endif
     if (st != 0 || last) break;
   }
   return st;
 }
 
-// Block epilogue shared by both K3 kernels.
-__device__ inline void k3_finish(const CompBlock& C, uint32_t ci, CompState* cstate, FrameState* fstate, int st,
-                                 const uint32_t rep[3]) {
-  if (st) {
-    key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
-    cstate[ci].stop = 1;
-  } else {
-    cstate[ci].rep_out[0] = rep[0];
-    cstate[ci].rep_out[1] = rep[1];
-    cstate[ci].rep_out[2] = rep[2];
-  }
+// The same chain with the bitstream window loaded two steps ahead: a
+// 24-byte window ending at the byte of pos_{i+1} covers every bit steps
+// i+1 and i+2 read (each step reads at most 63 extra + 27 state bits), so a
+// window load has a whole step more to land.
+struct Win6 {
+  uint32_t w0, w1, w2, w3, w4, w5;
+  int32_t wb;
+};
+typedef uint32_t u32x2ua __attribute__((ext_vector_type(2), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x2ua g_u32x2ua;
+__device__ inline Win6 win6_load(const uint8_t* s, int32_t m, int32_t pos) {
+  const int32_t tb = (pos + 7) >> 3;
+  const int32_t o = max(tb - 24, m);
+  const u32x4ua v = *(g_u32x4ua*)(s + o);
+  const u32x2ua u = *(g_u32x2ua*)(s + o + 16);
+  Win6 w;
+  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w; w.w4 = u.x; w.w5 = u.y;
+  w.wb = o * 8;
+  return w;
+}
+__device__ inline uint32_t win6_bits(const Win6& w, int32_t p, uint32_t S) {
+  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
+  const uint32_t k = y >> 5;
+  uint32_t lo = k == 0 ? w.w0 : w.w1;
+  uint32_t hi = k == 0 ? w.w1 : w.w2;
+  lo = k >= 2 ? w.w2 : lo;
+  hi = k >= 2 ? w.w3 : hi;
+  lo = k >= 3 ? w.w3 : lo;
+  hi = k >= 3 ? w.w4 : hi;
+  lo = k >= 4 ? w.w4 : lo;
+  hi = k >= 4 ? w.w5 : hi;
+  lo = k >= 5 ? w.w5 : lo;
+  hi = k >= 5 ? 0u : hi;
+  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
 }
 
-// K3 with the tables in HBM (L2-resident), no LDS: runs beside zd_k_sequences
-// on a second stream so the SIMDs the LDS-bound kernel leaves idle decode
-// more blocks (the split is LaunchArgs::k3_lds_blocks).
-constexpr int K3G_LANES = 64;
-__global__ __launch_bounds__(K3G_LANES) void zd_k_sequences_hbm(const uint8_t* __restrict__ src,
-                                                                const CompBlock* __restrict__ comp,
-                                                                CompState* cstate, FrameState* fstate,
-                                                                const uint32_t* __restrict__ list, uint32_t n_list,
-                                                                const uint16_t* __restrict__ fses,
-                                                                uint64_t* __restrict__ seqs) {
-  const uint32_t li = blockIdx.x * K3G_LANES + threadIdx.x;
-  if (li >= n_list) return;
-  const uint32_t ci = list[li];
-  const CompBlock C = comp[ci];
-  const uint64_t key0 = fstate[C.frame].key;
-  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
-  int al[3];
-  const uint16_t* g[3];
-  for (int k = 0; k < 3; k++) {
-    const uint32_t s = (uint32_t)C.tab_src[k];
-    al[k] = cstate[s].al[k];
-    g[k] = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+template <typename TP, bool K3_SYM>
+__device__ int seq_chain2(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
+                          int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
+  if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return ZD_E_NULL_BYTE;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
+  const int32_t A = all + alo + alm;
+  if (A > pos) return ZD_E_NOT_ENOUGH_BITS;
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-24);
+  const int32_t pos0 = pos;
+  const Win6 wi = win6_load(bs, m, pos);         // the init read
+  const uint32_t v0 = win6_bits(wi, pos, (uint32_t)A);
+  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
+  pos -= A;
+  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
+  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
+  // The loop entry sees the same memory-op order as its back edge (window,
+  // store, window, store), so the wait for a window two steps old is
+  // vmcnt(4), not a drain: step 0's window is loaded again for that.
+  Win6 wa = win6_load(bs, m, pos0);              // step 0 (covers pos0 - A - 90)
+  asm volatile("" ::: "memory");
+  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+  Win6 wb = win6_load(bs, m, pos);               // step 1
+  asm volatile("" ::: "memory");
+  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+  int st = 0;
+  uint32_t i = 0;
+  // one step reading window `use`, loading the window two steps ahead into
+  // `use`.  Both steps of an iteration run on every lane (no branch between
+  // them, so the loop entry keeps one memory-op order): a lane that finished
+  // in the first keeps its status and stores its second record into the
+  // block's spare slot.
+  auto step = [&](Win6& use, bool live) -> bool {
+    uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
+    if (K3_SYM) {
+      eLL = k3_entry(eLL, 0);
+      eOF = k3_entry(eOF, 1);
+      eML = k3_entry(eML, 2);
+    }
+    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
+    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
+    const uint32_t E = ((eLL >> 10) & 31) + ((eML >> 10) & 31) + ((eOF >> 10) & 31);
+    const bool codemax = ((eLL | eML | eOF) & K3_BAD) != 0;
+    const bool last = i + 1 >= n;
+    const uint32_t S = last ? 0 : nbL + nbM + nbO;
+    const int sst = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : ((int32_t)(E + S) > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
+    st = live ? sst : st;
+    const int32_t p2 = pos - (int32_t)E;
+    const uint32_t v = win6_bits(use, p2, S);
+    pos = p2 - (int32_t)S;
+    use = win6_load(bs, m, pos);                   // for step i + 2
+    const uint32_t vO = __builtin_amdgcn_ubfe(v, 0, nbO), vM = __builtin_amdgcn_ubfe(v, nbO, nbM);
+    const uint32_t vL = v >> (nbO + nbM);
+    sLL = (nsL << nbL) + vL - TL;
+    sML = (nsM << nbM) + vM - TM;
+    sOF = (nsO << nbO) + vO - TO;
+    asm volatile("" ::: "memory");
+    k3_store(out + (live ? i + 1 : n), (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+    i++;
+    return !live || sst != 0 || last;
+  };
+  for (;;) {
+    const bool d1 = step(wa, true);
+    const bool d2 = step(wb, !d1);
+    if (d2) break;
   }
-  const CompState cs = cstate[ci];
-  uint32_t rep[3];
-  rep_init(rep);
-  const int st = seq_block<g_u16*>(src + C.src + cs.bs_off, cs.bs_size, (uintptr_t)src, (g_u16*)g[0], (g_u16*)g[2],
-                                   (g_u16*)g[1], al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
-  k3_finish(C, ci, cstate, fstate, st, rep);
+  return st;
+}
+
+__device__ inline void k3_fail(const CompBlock& C, uint32_t ci, CompState* cstate, FrameState* fstate, int st) {
+  key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
+  cstate[ci].stop = 1;
 }
 
 __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __restrict__ src,
                                                            const CompBlock* __restrict__ comp, CompState* cstate,
                                                            FrameState* fstate, const uint32_t* __restrict__ list,
                                                            uint32_t n_list, const uint16_t* __restrict__ fses,
-                                                           uint64_t* __restrict__ seqs) {
+                                                           uint64_t* __restrict__ recs) {
   __shared__ __attribute__((aligned(16))) uint16_t tabs[K3_LANES * K3_TAB];
   const int lane = threadIdx.x;
   const uint32_t li = blockIdx.x * K3_LANES + lane;
@@ -827,23 +948,31 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
       g[k] = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
     }
   }
-  // tables -> LDS (every lane its own three), unless some lane needs AL 9 offsets
+  // tables -> LDS in the chain format (every lane its own three), unless
+  // some lane needs AL 9 offsets
   const bool deep = act && al[1] > 8;
   const bool use_lds = __ballot(deep) == 0;      // the workgroup is one wave
   lds_u16* mine = (lds_u16*)tabs + lane * K3_TAB;
   if (use_lds && act) {
-    const int cnt[3] = {1 << al[0], 1 << al[1], 1 << al[2]};
     const int dst[3] = {0, K3_TL + K3_TM, K3_TL};     // LL | ML | OF in LDS
     for (int k = 0; k < 3; k++) {
-      if (cnt[k] >= 8) {
+      const int cnt = 1 << al[k];
+      if (cnt >= 8) {
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         typedef __attribute__((address_space(1))) const u32x4 g_u4;
         typedef __attribute__((address_space(3))) u32x4 l_u4;
         g_u4* s4 = (g_u4*)g[k];
         l_u4* d4 = (l_u4*)(mine + dst[k]);
-        for (int e = 0; e < cnt[k] / 8; e++) d4[e] = s4[e];
+        for (int e = 0; e < cnt / 8; e++) {
+          u32x4 v = s4[e];
+          v.x = k3_entry(v.x & 0xFFFF, k) | (k3_entry(v.x >> 16, k) << 16);
+          v.y = k3_entry(v.y & 0xFFFF, k) | (k3_entry(v.y >> 16, k) << 16);
+          v.z = k3_entry(v.z & 0xFFFF, k) | (k3_entry(v.z >> 16, k) << 16);
+          v.w = k3_entry(v.w & 0xFFFF, k) | (k3_entry(v.w >> 16, k) << 16);
+          d4[e] = v;
+        }
       } else {
-        for (int e = 0; e < cnt[k]; e++) mine[dst[k] + e] = ((g_u16*)g[k])[e];
+        for (int e = 0; e < cnt; e++) mine[dst[k] + e] = (uint16_t)k3_entry(((g_u16*)g[k])[e], k);
       }
     }
   }
@@ -852,18 +981,15 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
   const CompState cs = cstate[ci];
   const uint8_t* blk = src + C.src;
   const uintptr_t lo = (uintptr_t)src;
-  uint32_t rep[3];
-  rep_init(rep);
   int st;
   if (use_lds)
-    st = seq_block<const lds_u16*>(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM,
-                                   al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
+    st = K3_CHAIN<const lds_u16*, false>(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM,
+                                          al[0], al[1], al[2], C.nseq, recs + C.seq_out);
   else
-    st = seq_block<g_u16*>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2],
-                           (g_u16*)g[1], al[0], al[1], al[2], C.nseq, seqs + C.seq_out, rep);
-  k3_finish(C, ci, cstate, fstate, st, rep);
+    st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0],
+                                 al[1], al[2], C.nseq, recs + C.seq_out);
+  if (st) k3_fail(C, ci, cstate, fstate, st);
 }
-
 // ---------------------------------------------------------------------------
 // K4: execute (decoding_context.rs:50-106 + block.rs:74-99), one frame per
 // wave, one sequence per lane, 64 sequences per batch.  A frame that decodes
@@ -920,6 +1046,22 @@ __device__ inline uint32_t scan_incl_u32(uint32_t x, int lane) {
     if (lane >= d) x += y;
   }
   return x;
+}
+
+__device__ inline uint64_t readlane_u64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+// Repeat offsets after `cnt` fresh lanes ending at lane end - 1 pushed their
+// values on top of (r0, r1, r2) (decoding_context.rs:67-71 applied cnt times).
+__device__ inline void rep_push(uint64_t val, int cnt, int end, uint64_t r0, uint64_t r1, uint64_t r2, uint64_t* a0,
+                                uint64_t* a1, uint64_t* a2) {
+  uint64_t b0 = r0, b1 = r1, b2 = r2;
+  if (cnt >= 1) { b0 = readlane_u64(val, end - 1); b1 = r0; b2 = r1; }
+  if (cnt >= 2) { b1 = readlane_u64(val, end - 2); b2 = r0; }
+  if (cnt >= 3) b2 = readlane_u64(val, end - 3);
+  *a0 = b0; *a1 = b1; *a2 = b2;
 }
 
 struct K4 {
@@ -1046,9 +1188,11 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
                                                    const CompBlock* __restrict__ comp,
                                                    const CompState* __restrict__ cstate,
                                                    const uint8_t* __restrict__ lits,
-                                                   const uint64_t* __restrict__ seqs) {
+                                                   const uint64_t* __restrict__ seqs,
+                                                   const uint16_t* __restrict__ fses) {
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
+  __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
   const int lane = threadIdx.x;
   const uint32_t f = blockIdx.x;
   const FrameDesc F = frames[f];
@@ -1100,21 +1244,89 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
     uint64_t lit_cursor = 0;
     const uint64_t* SQ = seqs + C.seq_out;
     const uint32_t n = C.nseq;
+    const bool direct = C.seq_direct != 0;
+    // the block's LL/OF/ML symbols (K1's sym entries, zd_common.h) -> LDS
+    const uint8_t* bsp = src + C.src + CS.bs_off;
+    if (n && !direct) {
+      for (int k = 0; k < 3; k++) {
+        const uint32_t s = (uint32_t)C.tab_src[k];
+        const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+        const int cnt = 1 << cstate[s].al[k];
+        for (int e = lane; e < cnt; e += 64) stab[k][e] = (uint8_t)(g[e] & 63);
+      }
+      __syncthreads();
+    }
     uint64_t nxt = lane < (int)n ? SQ[lane] : 0;
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
       const uint32_t i = s0 + lane;
       const bool valid = i < n;
       const uint64_t sq = nxt;
       nxt = (i + 64 < n) ? SQ[i + 64] : 0;       // next batch's records, in flight
-      const uint32_t ll = valid ? seq_ll(sq) : 0, ml = valid ? seq_ml(sq) : 0;
-      // decode_offset (decoding_context.rs:50-75): K3's code against the block's incoming offsets
-      uint64_t off = 0;
-      const int derr = valid ? off_resolve(seq_off(sq), rep, &off) : 0;
+      // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
+      // K3 recorded the bit position and the three states; OF, ML, LL extra
+      // bits are read here, in that order, below the position.
+      uint32_t ll = 0, ml = 0, ofv = 0;
+      bool giant = false;
+      if (valid) {
+        if (direct) {
+          ll = seq_ll(sq); ml = seq_ml(sq); ofv = seq_off(sq);
+          giant = ofv == DIRECT_GIANT;
+        } else {
+          const int32_t pos = (int32_t)(uint32_t)sq;
+          const uint32_t stt = (uint32_t)(sq >> 32);
+          const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
+          uint32_t llbase, llb, mlbase, mlb;
+          ll_code(llc, &llbase, &llb);
+          ml_code(mlc, &mlbase, &mlb);
+          uint64_t t = winu_top(winu_load(bsp, (uintptr_t)src, pos), 0);
+          const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
+          ofv = (1u << ofc) + ob;
+          ml = mlbase + mb;
+          ll = llbase + lb;
+        }
+      }
       k4_room(X);
       const uint32_t tot = ll + ml;
       const uint32_t inc_tot = scan_incl_u32(tot, lane);
       const uint32_t inc_ll = scan_incl_u32(ll, lane);
       const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
+      const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= X.space() - 16);
+      const uint32_t k = (uint32_t)__popcll(fitm);
+      const int kk = k ? (int)k : 1;                   // lanes this batch executes
+      // decode_offset (decoding_context.rs:50-75): fresh offsets (> 3) are
+      // direct; the rare repeat codes walk the batch in order on the scalar
+      // unit, each from the state the fresh offsets before it left.
+      const bool fresh = ofv > 3;
+      const uint64_t val = giant ? OFF_HUGE : (uint64_t)ofv - 3;
+      uint64_t off = val;
+      int derr = 0;
+      uint64_t rm = __ballot(valid && !fresh && lane < kk);
+      uint64_t r0 = rep[0], r1 = rep[1], r2 = rep[2];   // state after lane `prev`
+      int prev = -1;
+      while (rm) {
+        const int ri = __ffsll((long long)rm) - 1;
+        rm &= rm - 1;
+        uint64_t a0, a1, a2;
+        rep_push(val, ri - prev - 1, ri, r0, r1, r2, &a0, &a1, &a2);
+        const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)ofv, ri);
+        const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)ll, ri);
+        uint64_t o = 0;
+        int e = 0;
+        if (oi == 0) {
+          e = ZD_E_NULL_OFFSET;
+        } else {
+          const uint32_t idx = oi - (li != 0 ? 1u : 0u);
+          if (idx == 0) { o = a0; }
+          else if (idx == 1) { o = a1; a1 = a0; a0 = o; }
+          else if (idx == 2) { o = a2; a2 = a1; a1 = a0; a0 = o; }
+          else if (a0 == 0) { e = ZD_E_REF_PANIC; }     // usize underflow of offsets[0] -= 1
+          else { o = a0 - 1; a2 = a1; a1 = a0; a0 = o; }
+        }
+        if (lane == ri) { off = o; derr = e; }
+        r0 = a0; r1 = a1; r2 = a2;
+        prev = ri;
+        if (e) break;                                  // the frame stops at this sequence
+      }
       // checks (decoding_context.rs:86-90, D9)
       const uint64_t before = (uint64_t)X.pos + opos;
       const bool dbad = valid && derr != 0;
@@ -1122,8 +1334,6 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
                                           off > before + ll);
       const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
       const uint64_t badm = __ballot(dbad || imp || panic);
-      const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= X.space() - 16);
-      const uint32_t k = (uint32_t)__popcll(fitm);
       if (badm) {
         const int b = __ffsll((long long)badm) - 1;
         if ((uint32_t)b < (k ? k : 1u)) {
@@ -1140,6 +1350,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
           err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN);
           break;
         }
+        rep_push(val, 0 - prev, 1, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
         lit_cursor += ll0;
         s0 += 1;
         if (s0 < n) nxt = (s0 + lane < n) ? SQ[s0 + lane] : 0;
@@ -1186,6 +1397,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
         done |= __ballot(mine);
         __syncthreads();
       }
+      rep_push(val, (int)k - 1 - prev, (int)k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);   // state after lane k - 1
       lit_cursor += L;
       X.pos += T;
       s0 += k;
@@ -1193,12 +1405,6 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       k4_flush(X, false);
     }
     if (err_key != KEY_NONE) break;
-    // repeat offsets after the block
-    if (n) {
-      uint64_t nr[3];
-      for (int kk = 0; kk < 3; kk++) (void)off_resolve(CS.rep_out[kk], rep, &nr[kk]);
-      rep[0] = nr[0]; rep[1] = nr[1]; rep[2] = nr[2];
-    }
     // leftover literals (decoding_context.rs:101-103)
     if (lit_cursor < nl && !k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, nl - lit_cursor))
       err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_OUT_OF_DOMAIN);
@@ -1245,42 +1451,23 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   hipStream_t s = a.stream;
   hipError_t e;
   if (a.events) if ((e = hipEventRecord(a.events[0], s)) != hipSuccess) return e;
-  if (a.n_tables)
+  if (a.n_tables && (a.kmask & 1))
     hipLaunchKernelGGL(zd_k_tables, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
                        a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
-  if (a.n_huf)
+  if (a.n_huf && (a.kmask & 2))
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
-  if (a.n_seq) {
-    // blocks [0, n_lds) on the LDS kernel, the rest on the HBM-table kernel
-    // on the aux stream, concurrently
-    const uint32_t* list = (const uint32_t*)(ws + W.list_seq);
-    uint32_t n_lds = a.n_seq;
-    if (a.aux && a.k3_lds_frac < 1.0f) {
-      n_lds = (uint32_t)((double)a.n_seq * a.k3_lds_frac) / K3_LANES * K3_LANES;
-      if (n_lds > a.n_seq) n_lds = a.n_seq;
-    }
-    const uint32_t n_hbm = a.n_seq - n_lds;
-    if (n_hbm) {
-      if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
-      hipLaunchKernelGGL(zd_k_sequences_hbm, dim3((n_hbm + K3G_LANES - 1) / K3G_LANES), dim3(K3G_LANES), 0, a.aux,
-                         a.src, comp, cstate, fstate, list + n_lds, n_hbm, (const uint16_t*)fses, seqs);
-    }
-    if (n_lds)
-      hipLaunchKernelGGL(zd_k_sequences, dim3((n_lds + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
-                         cstate, fstate, list, n_lds, (const uint16_t*)fses, seqs);
-    if (n_hbm) {
-      if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-    }
-  }
+  if (a.n_seq && (a.kmask & 4))
+    hipLaunchKernelGGL(zd_k_sequences, dim3((a.n_seq + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
+                       cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses,
+                       seqs);
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
-  if (a.n_frames)
+  if (a.n_frames && (a.kmask & 8))
     hipLaunchKernelGGL(zd_k_execute, dim3(a.n_frames), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
-                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs);
+                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
+                       (const uint16_t*)fses);
   if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
   return hipGetLastError();
 }

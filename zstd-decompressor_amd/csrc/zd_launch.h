@@ -16,11 +16,7 @@ struct LaunchArgs {
   uint32_t n_tables, n_huf, n_seq, n_frames;
   hipStream_t stream;
   hipEvent_t* events;      // optional: 5 events recorded around the 4 kernels
-  // K3 split: a fraction of the sequence blocks runs on the HBM-table kernel
-  // on `aux` (fork/join events), beside the LDS kernel on `stream`
-  hipStream_t aux;
-  hipEvent_t fork, join;
-  float k3_lds_frac;
+  uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
@@ -31,7 +27,6 @@ hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* 
                           const uint64_t* d_to, const uint64_t* d_len, uint32_t n, hipStream_t s);
 
 constexpr int N_KERNELS = 4;
-constexpr float K3_LDS_FRAC_DEFAULT = 1.0f;
 extern const char* const kKernelNames[N_KERNELS];
 
 }  // namespace zd

@@ -1,0 +1,114 @@
+"""Frame-sharded multi-GPU decode.
+
+Frames are independent: each gets a fresh DecodingContext (frame.rs:232-237)
+and the CLI only concatenates frame outputs (src/main.rs:43-53).  So ranks
+take contiguous frame ranges balanced by compressed bytes, each rank decodes
+its range into its own HBM with the batch plan (no collective on the data
+path), and the decoded ranges are gathered to rank 0 with point-to-point
+sends — RCCL over xGMI for device tensors (backend "nccl"), gloo on CPU.
+
+One process per GPU; torch.distributed must already be initialised by the
+caller (torchrun / init_process_group) when world > 1.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+
+def partition(sizes: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous [begin, end) item ranges, one per rank, cut where the
+    running sum of `sizes` crosses k/world of the total (every range is
+    non-empty while there are at least `world` items)."""
+    import bisect
+    n = len(sizes)
+    if world <= 0:
+        raise ValueError("world must be positive")
+    prefix = [0]
+    for s in sizes:
+        prefix.append(prefix[-1] + s)
+    total = prefix[-1]
+    cuts = [0]
+    for k in range(1, world):
+        # first item boundary whose prefix reaches k/world of the bytes
+        c = bisect.bisect_left(prefix, total * k / world)
+        if n >= world:                       # leave one item for each remaining rank
+            c = max(c, cuts[-1] + 1)
+            c = min(c, n - (world - k))
+        cuts.append(min(max(c, cuts[-1]), n))
+    cuts.append(n)
+    return [(cuts[k], cuts[k + 1]) for k in range(world)]
+
+
+def shard_of(frames: Sequence[dict], rank: int, world: int) -> Tuple[int, int, int, int]:
+    """(src_begin, src_end, frame_begin, frame_end) of this rank's frames, as
+    given by zstd_decompressor.batch.frames_index."""
+    ranges = partition([f["src_size"] for f in frames], world)
+    b, e = ranges[rank]
+    if b == e:
+        off = frames[b]["src_offset"] if b < len(frames) else (
+            frames[-1]["src_offset"] + frames[-1]["src_size"] if frames else 0)
+        return off, off, b, e
+    return frames[b]["src_offset"], frames[e - 1]["src_offset"] + frames[e - 1]["src_size"], b, e
+
+
+def gather_to_root(local: torch.Tensor, length: int, rank: int, world: int, group=None) -> Optional[torch.Tensor]:
+    """Concatenate every rank's first `length` bytes of `local` (uint8, 1-D) on
+    rank 0, in rank order.  Lengths are exchanged first (all_gather), then
+    each peer sends its range to rank 0 (point-to-point; over RCCL each send
+    rides the peer's own xGMI link to GPU 0).  Returns the concatenation on
+    rank 0 and None elsewhere."""
+    import torch.distributed as dist
+    if world == 1:
+        return local[:length]
+    dev = local.device
+    lens = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(lens, torch.tensor([length], dtype=torch.int64, device=dev), group=group)
+    lens = [int(t.item()) for t in lens]
+    if rank == 0:
+        out = torch.empty(sum(lens), dtype=torch.uint8, device=dev)
+        out[: lens[0]].copy_(local[: lens[0]])
+        off = lens[0]
+        reqs = []
+        for r in range(1, world):
+            if lens[r]:
+                reqs.append(dist.irecv(out[off: off + lens[r]], src=r, group=group))
+            off += lens[r]
+        for q in reqs:
+            q.wait()
+        return out
+    if length:
+        dist.send(local[:length].contiguous(), dst=0, group=group)
+    return None
+
+
+def decode_sharded(data: bytes, rank: int, world: int, device: torch.device, group=None,
+                   gather: bool = True):
+    """Decode this rank's share of the frames of `data` on `device` (one GPU
+    per rank) and optionally gather the whole output on rank 0.
+
+    Returns (status, local_output_tensor, local_length, gathered_or_None).
+    The status is this rank's zd_plan_results status (0 = OK)."""
+    from .batch import Plan, frames_index
+    frames, _, st, _ = frames_index(data)
+    if st != 0:
+        raise ValueError(f"frame index failed with status {st}")
+    sb, se, _, _ = shard_of(frames, rank, world)
+    part = data[sb:se]
+    length = 0
+    status = 0
+    local = torch.empty(1, dtype=torch.uint8, device=device)
+    if part:
+        plan = Plan(part)
+        cap = max(int(plan.info.out_bytes), 1)
+        d_src = torch.zeros(len(part) + 64, dtype=torch.uint8, device=device)
+        d_src[: len(part)].copy_(torch.frombuffer(bytearray(part), dtype=torch.uint8))
+        local = torch.empty(cap + 64, dtype=torch.uint8, device=device)
+        s = torch.cuda.current_stream(device).cuda_stream
+        plan.decode_async(d_src.data_ptr(), local.data_ptr(), cap, s)
+        torch.cuda.synchronize(device)
+        status, length, _, _, _ = plan.results(local.data_ptr(), s)
+        plan.close()
+    gathered = gather_to_root(local, length, rank, world, group) if gather else None
+    return status, local, length, gathered
