@@ -105,6 +105,69 @@ ZD_HD inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >> 17) & 0x3FFFF
 ZD_HD inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 35); }
 
 // ---------------------------------------------------------------------------
+// Repeat-offset codes (u32) for resolving decode_offset (decoding_context.rs:
+// 50-75) by a parallel scan (K4F).  A segment of sequences maps the three
+// incoming repeat offsets to three outgoing ones, each either a concrete
+// value or "incoming slot j minus d" (d decrements of the `3, ll == 0` rule):
+//   v <  OFF_SYM                    concrete offset v
+//   OFF_SYM + (j << 24) + d         incoming rep[j] - d
+//   OFF_GIANT                       an offset >= 2^28: past any frame K4F
+//                                   decodes (ImpossibleValue when used)
+//   OFF_NULL                        offset_value 0 (NullOffsetError)
+//   OFF_UNDERFLOW                   usize underflow of rep0 - 1 (ZD_E_REF_PANIC)
+// Maps compose with rc_apply, so the state before every thread's sequences
+// is an exclusive scan of the threads' maps.
+// ---------------------------------------------------------------------------
+constexpr uint32_t OFF_SYM = 1u << 28;
+constexpr uint32_t OFF_GIANT = (1u << 29) - 3;
+constexpr uint32_t OFF_NULL = (1u << 29) - 2;
+constexpr uint32_t OFF_UNDERFLOW = (1u << 29) - 1;
+
+ZD_HD inline void rep_ident(uint32_t r[3]) { r[0] = OFF_SYM; r[1] = OFF_SYM | (1u << 24); r[2] = OFF_SYM | (2u << 24); }
+ZD_HD inline uint32_t rep_code(uint64_t v) { return v < OFF_SYM ? (uint32_t)v : OFF_GIANT; }
+ZD_HD inline uint64_t rep_value(uint32_t c) { return c < OFF_SYM ? (uint64_t)c : OFF_HUGE; }
+ZD_HD inline uint32_t rep_dec1(uint32_t v) {
+  // giant stays giant; after an underflow the reference stopped; a symbolic
+  // value counts one more decrement; 0 underflows (selects, no branches)
+  uint32_t t = v >= OFF_SYM ? v + 1 : v - 1;
+  t = v == 0 ? OFF_UNDERFLOW : t;
+  return v >= OFF_GIANT ? v : t;
+}
+// decode_offset on codes: updates r, returns the offset code.  idx = the
+// repeat slot an offset_value <= 3 names (RFC 8878 3.1.1.5), 3 = rep0 - 1.
+ZD_HD inline uint32_t rep_step(uint32_t r[3], uint32_t ofv, uint32_t ll) {
+  const uint32_t r0 = r[0], r1 = r[1], r2 = r[2];
+  const bool fresh = ofv > 3;
+  const uint32_t idx = ofv - (ll != 0 ? 1u : 0u);
+  uint32_t rep = idx == 0 ? r0 : r1;
+  rep = idx >= 2 ? r2 : rep;
+  rep = idx == 3 ? rep_dec1(r0) : rep;
+  const uint32_t v = ofv - 3;
+  const uint32_t n0 = fresh ? (v >= OFF_SYM ? OFF_GIANT : v) : rep;
+  const uint32_t n1 = (!fresh && idx == 0) ? r1 : r0;
+  const uint32_t n2 = (!fresh && idx <= 1) ? r2 : r1;
+  const bool null = ofv == 0;
+  r[0] = null ? r0 : n0;
+  r[1] = null ? r1 : n1;
+  r[2] = null ? r2 : n2;
+  return null ? OFF_NULL : n0;
+}
+// code b evaluated with the incoming slots a[3] (which may be codes too)
+ZD_HD inline uint32_t rc_apply(uint32_t b, const uint32_t a[3]) {
+  if (b < OFF_SYM || b >= OFF_GIANT) return b;
+  const uint32_t j = (b - OFF_SYM) >> 24, d = (b - OFF_SYM) & 0xFFFFFFu;
+  const uint32_t x = j == 0 ? a[0] : (j == 1 ? a[1] : a[2]);
+  if (x >= OFF_GIANT) return x;
+  if (x >= OFF_SYM) return x + d;
+  return x >= d ? x - d : OFF_UNDERFLOW;
+}
+// map b after map a (a's outputs feed b's inputs)
+ZD_HD inline void rc_compose(const uint32_t a[3], uint32_t b[3]) {
+  const uint32_t c0 = rc_apply(b[0], a), c1 = rc_apply(b[1], a), c2 = rc_apply(b[2], a);
+  b[0] = c0; b[1] = c1; b[2] = c2;
+}
+
+// ---------------------------------------------------------------------------
 // Error keys.  The reference parses every block of a frame (tables included)
 // before decoding any (frame.rs:198-230 then 232-260), and stops at the first
 // error in each phase.  A key orders errors the same way; per frame we keep
@@ -186,6 +249,8 @@ struct FrameDesc {
   uint64_t out_len0;       // bytes already produced before this launch (context API)
   uint32_t first_block;    // into BlockRec[]
   uint32_t nblocks;        // blocks to execute (0 for frames skipped by parse errors)
+  uint32_t lds;            // 1: executed by K4F (whole frame in LDS), 0: by the streaming K4
+  uint32_t _pad;
 };
 
 struct FrameState {
@@ -197,7 +262,7 @@ struct FrameState {
 // Workspace carve-up, all offsets in bytes from the workspace base.
 struct Workspace {
   uint64_t comp, comp_state, blocks, frames, frame_state;
-  uint64_t list_tables, list_huf, list_seq;   // u32 work lists
+  uint64_t list_tables, list_huf, list_seq, list_k4f;   // u32 work lists
   uint64_t lits, seqs, luts, fses;
   uint64_t total;
 };

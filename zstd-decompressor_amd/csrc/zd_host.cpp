@@ -313,7 +313,7 @@ struct zd_plan {
   std::vector<BlockRec> blocks;
   std::vector<FrameDesc> fdesc;
   std::vector<FrameState> fstate0;
-  std::vector<uint32_t> list_tables, list_huf, list_seq;
+  std::vector<uint32_t> list_tables, list_huf, list_seq, list_k4f;
   std::vector<uint64_t> frame_cap_off;   // output offset per frame (capacity layout)
   zd_plan_info info{};
   Workspace W{};
@@ -341,7 +341,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   uint64_t lits = 0, nseq_total = 0, nrec = 0, out_off = 0;
   uint32_t lut_slots = 0, fse_slots = 0;
   bool exact = true;
-  P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear();
+  P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear();
   P->frame_cap_off.clear();
   for (size_t fi = 0; fi < P->frames.size(); fi++) {
     HostFrame& hf = P->frames[fi];
@@ -446,6 +446,12 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
       fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
     fd.out = out_off;
     fd.out_cap = cap;
+    // K4F (whole frame resident in LDS) is an experimental executor, off by
+    // default (slower than the streaming K4 on C4); ZD_K4F=1 routes
+    // every frame that fits to it
+    static const bool k4f_on = getenv("ZD_K4F") && atoi(getenv("ZD_K4F")) == 1;
+    fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
+    if (fd.lds) P->list_k4f.push_back((uint32_t)fi);
     P->frame_cap_off.push_back(out_off);
     out_off += cap;
     P->fdesc.push_back(fd);
@@ -463,6 +469,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.list_tables = carve(4 * std::max<size_t>(P->list_tables.size(), 1));
   W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
   W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
+  W.list_k4f = carve(4 * std::max<size_t>(P->list_k4f.size(), 1));
   W.lits = carve(lits + 64);
   W.seqs = carve(8 * nrec + 64);
   W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
@@ -494,6 +501,7 @@ int upload_plan(zd_plan* P) {
   if (int r = up(P->W.list_tables, P->list_tables.data(), P->list_tables.size() * 4)) return r;
   if (int r = up(P->W.list_huf, P->list_huf.data(), P->list_huf.size() * 4)) return r;
   if (int r = up(P->W.list_seq, P->list_seq.data(), P->list_seq.size() * 4)) return r;
+  if (int r = up(P->W.list_k4f, P->list_k4f.data(), P->list_k4f.size() * 4)) return r;
   if (!P->info.out_exact) {
     P->staging_bytes = P->info.out_bytes;
     HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
@@ -661,6 +669,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_huf = (uint32_t)P->list_huf.size();
   a.n_seq = (uint32_t)P->list_seq.size();
   a.n_frames = (uint32_t)P->fdesc.size();
+  a.n_k4f = (uint32_t)P->list_k4f.size();
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
@@ -853,6 +862,7 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   a.n_huf = (uint32_t)P->list_huf.size();
   a.n_seq = (uint32_t)P->list_seq.size();
   a.n_frames = 1;
+  a.n_k4f = (uint32_t)P->list_k4f.size();
   a.stream = nullptr;
   if (launch_pipeline(a) != hipSuccess) return fin(ZD_E_HIP);
   if (hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
@@ -1058,6 +1068,7 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   LaunchArgs a{};
   a.src = d_src; a.src_size = nlits; a.out = c->d_out; a.ws = P.d_ws; a.W = P.W;
   a.n_frames = 1;
+  a.n_k4f = (uint32_t)P.list_k4f.size();
   if (launch_pipeline(a) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
   FrameState st{};
   if (hipMemcpy(&st, P.d_ws + P.W.frame_state, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return fin(ZD_E_HIP);

@@ -1196,6 +1196,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
   const int lane = threadIdx.x;
   const uint32_t f = blockIdx.x;
   const FrameDesc F = frames[f];
+  if (F.lds) return;                             // K4F executes this frame
   FrameState* S = &fstate[f];
   const uint64_t key0 = S->key;
   if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
@@ -1423,6 +1424,450 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
 }
 
 // ---------------------------------------------------------------------------
+// K4F: execute with the whole frame resident in LDS (decoding_context.rs:
+// 50-106 + block.rs:74-99), for frames whose output fits K4F_CAP (every
+// 128 KiB single-segment frame).  One 1024-thread workgroup per frame; a
+// block's sequences go in chunks of K4F_T x K4F_KC, each thread owning
+// K4F_KC consecutive sequences:
+//   values   records (K3) -> symbols (LDS) + extra bits (bitstream window)
+//   offsets  decode_offset as an exclusive scan of the threads' repeat maps
+//            (zd_common.h rep codes), then a concrete walk per thread
+//   places   exclusive scans of literal/total lengths
+//   checks   the first failing sequence of the chunk (min over threads),
+//            reference order: decode_offset, ImpossibleValue, zero offset
+//   literals every run copied into the LDS frame at once
+//   matches  in rounds: a match copies once every byte of its source is
+//            written (1 bit per frame byte in LDS); each round completes at
+//            least the earliest pending match, typically 3-4 rounds in all
+// The frame never leaves LDS until it is complete: no HBM re-reads of match
+// sources, and one coalesced write of the frame at the end.
+// ---------------------------------------------------------------------------
+constexpr int K4F_T = 1024;
+constexpr int K4F_W = K4F_T / 64;
+#ifndef ZD_K4F_KC
+#define ZD_K4F_KC 4
+#endif
+constexpr int K4F_KC = ZD_K4F_KC;
+constexpr uint32_t K4F_CHUNK = (uint32_t)K4F_T * K4F_KC;
+constexpr uint32_t K4F_LIST = 1024;
+struct K4FShared {
+  uint8_t buf[K4F_CAP + 64];
+  uint32_t bits[K4F_CAP / 32 + 4];     // 1 = byte written (or not a pending match byte)
+  uint8_t stab[3][FSE_TAB];            // LL | OF | ML symbols of the block
+  uint32_t wmap[K4F_W][3];             // per-wave repeat maps, then their exclusive prefixes
+  uint32_t wsum[K4F_W][2];             // per-wave length sums, then their exclusive prefixes
+  uint64_t rep[2][3];                  // concrete repeat offsets into a chunk (double-buffered)
+  unsigned long long err, lim;         // first failing sequence of the chunk
+  uint32_t tot[2];                     // chunk output / literal totals
+  uint32_t lq[K4F_LIST], lo[K4F_LIST], lm[K4F_LIST];   // matches left after the parallel round, in order
+};
+
+__device__ inline void k4f_bits_and(uint32_t* bits, uint32_t p, uint32_t n, bool set) {
+  uint32_t w = p >> 5, e = p + n;
+  while (p < e) {
+    const uint32_t lo = p & 31, hi = min(32u, lo + (e - p));
+    const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1)) & ~((1u << lo) - 1);
+    if (set) atomicOr(&bits[w], m);
+    else atomicAnd(&bits[w], ~m);
+    p += hi - lo;
+    w++;
+  }
+}
+__device__ inline bool k4f_bits_all(const uint32_t* bits, uint32_t p, uint32_t n) {
+  const uint32_t e = p + n;
+  while (p < e) {
+    const uint32_t lo = p & 31, hi = min(32u, lo + (e - p));
+    const uint32_t m = (hi == 32 ? ~0u : ((1u << hi) - 1)) & ~((1u << lo) - 1);
+    if ((bits[p >> 5] & m) != m) return false;
+    p += hi - lo;
+  }
+  return true;
+}
+// wave-inclusive scan of a repeat map (lanes < d keep theirs)
+__device__ inline void k4f_scan_map(uint32_t m[3], int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t a[3];
+    a[0] = (uint32_t)__shfl_up((int)m[0], d, 64);
+    a[1] = (uint32_t)__shfl_up((int)m[1], d, 64);
+    a[2] = (uint32_t)__shfl_up((int)m[2], d, 64);
+    if (lane >= d) rc_compose(a, m);
+  }
+}
+
+// One match: ml bytes at q from q - o (overlap-safe, decoding_context.rs:95-98).
+__device__ inline void k4f_match(l_u8* buf, uint32_t q, uint32_t o, uint32_t mk) {
+  l_u8* d = buf + q;
+  const l_u8* sp = buf + q - o;
+  if (o >= 16) {
+    for (uint32_t x = 0; x < mk; x += 16) sts_n(d + x, lds16(sp + x), mk - x);
+  } else {                                        // small period: 16 bytes bytewise, then 16-byte steps
+    const uint32_t m16 = o * ((16 + o - 1) / o);
+    const uint32_t head = mk < 16 ? mk : 16;
+    uint32_t r = 0;
+    for (uint32_t x = 0; x < head; x++) {
+      d[x] = sp[r];
+      r = r + 1 == o ? 0 : r + 1;
+    }
+    for (uint32_t x = 16; x < mk; x += 16) sts_n(d + x, lds16(d + x - m16), mk - x);
+  }
+}
+struct K4FShared;
+// The matches the parallel round left, in sequence order, by one wave: 64 at
+// a time in frontier rounds (a match copies once its source lies below the
+// first unfinished match of the batch; everything before the batch is done).
+template <typename SH>
+__device__ inline void k4f_ordered(SH& L, uint32_t cnt, int lane) {
+  for (uint32_t b = 0; b < cnt; b += 64) {
+    const uint32_t i = b + lane;
+    const bool v = i < cnt;
+    const uint32_t q = v ? L.lq[i] : 0, o = v ? L.lo[i] : 1, mk = v ? L.lm[i] : 0;
+    const uint32_t shi = q - o + (o < mk ? o : mk);
+    uint64_t done = __ballot(!v);
+    while (done != ~0ull) {
+      const int U = __ffsll((long long)~done) - 1;
+      const uint32_t qU = (uint32_t)__builtin_amdgcn_readlane((int)q, U);
+      const bool mine = !((done >> lane) & 1) && (lane == U || shi <= qU);
+      if (mine) k4f_match((l_u8*)L.buf, q, o, mk);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      done |= __ballot(mine);
+    }
+  }
+}
+
+__global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restrict__ src, uint8_t* outbase,
+                                                          const FrameDesc* __restrict__ frames, FrameState* fstate,
+                                                          const BlockRec* __restrict__ blocks,
+                                                          const CompBlock* __restrict__ comp,
+                                                          const CompState* __restrict__ cstate,
+                                                          const uint8_t* __restrict__ lits,
+                                                          const uint64_t* __restrict__ seqs,
+                                                          const uint16_t* __restrict__ fses,
+                                                          const uint32_t* __restrict__ flist) {
+  __shared__ __attribute__((aligned(16))) K4FShared L;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t f = flist[blockIdx.x];
+  const FrameDesc F = frames[f];
+  FrameState* S = &fstate[f];
+  const uint64_t key0 = S->key;
+  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
+  const uint32_t cap = (uint32_t)(F.out_cap < K4F_CAP ? F.out_cap : K4F_CAP);
+  for (uint32_t x = t; x < K4F_CAP / 32 + 4; x += K4F_T) L.bits[x] = ~0u;
+  if (t == 0) { L.rep[0][0] = S->rep[0]; L.rep[0][1] = S->rep[1]; L.rep[0][2] = S->rep[2]; }
+  int rb = 0;                                     // which rep buffer holds the current state
+  uint32_t pos = 0;                               // frame bytes produced (uniform)
+  uint64_t err_key = KEY_NONE;
+  __syncthreads();
+
+  for (uint32_t j = 0; j < F.nblocks; j++) {
+    const BlockRec B = blocks[F.first_block + j];
+    if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
+    if (B.type == 5) continue;
+    if (B.type != 2) {                            // raw / RLE / skippable payload
+      if ((uint64_t)pos + B.size > cap) { err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN); break; }
+      const uint32_t fill = B.rle * 0x01010101u;
+      const u32x4 f4 = (u32x4){fill, fill, fill, fill};
+      for (uint32_t x = 16 * t; x < B.size; x += 16 * K4F_T) {
+        const u32x4 v = B.type == 1 ? f4 : ldg16(src + B.src + x);
+        sts_n((l_u8*)L.buf + pos + x, v, min(16u, B.size - x));
+      }
+      pos += B.size;
+      __syncthreads();
+      continue;
+    }
+    const CompBlock C = comp[B.comp];
+    const CompState CS = cstate[B.comp];
+    if (CS.stop) break;
+    const uint8_t* lsrc = nullptr;
+    uint32_t lfill = 0, nl;
+    if (C.lit_type == LIT_RAW) { lsrc = src + C.src + C.lit_data; nl = C.lit_regen; }
+    else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle * 0x01010101u; nl = C.lit_regen; }
+    else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
+    const u32x4 f4 = (u32x4){lfill, lfill, lfill, lfill};
+    const uint32_t n = C.nseq;
+    const bool direct = C.seq_direct != 0;
+    const uint64_t* SQ = seqs + C.seq_out;
+    const uint8_t* bsp = src + C.src + CS.bs_off;
+    if (n && !direct) {
+      for (int k = 0; k < 3; k++) {
+        const uint32_t s = (uint32_t)C.tab_src[k];
+        const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+        const int cnt = 1 << cstate[s].al[k];
+        for (int e = t; e < cnt; e += K4F_T) L.stab[k][e] = (uint8_t)(g[e] & 63);
+      }
+    }
+    uint32_t lit_cursor = 0;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += K4F_CHUNK) {
+      const uint32_t cn = min(K4F_CHUNK, n - c0);
+      const uint32_t b0 = (uint32_t)t * K4F_KC;
+#ifdef ZD_K4F_PROF
+      uint64_t tp[8]; int np = 0, rounds = 0;
+      tp[np++] = __builtin_amdgcn_s_memtime();
+#endif
+      uint32_t ll[K4F_KC], ml[K4F_KC], oc[K4F_KC];
+      // values (update_symbol_value, decoders/sequence.rs:41-55)
+#pragma unroll
+      for (int k = 0; k < K4F_KC; k++) {
+        ll[k] = 0; ml[k] = 0; oc[k] = 4;          // padding: no bytes, a fresh offset
+        if (b0 + k < cn) {
+          const uint64_t sq = SQ[c0 + b0 + k];
+          if (direct) {
+            ll[k] = seq_ll(sq); ml[k] = seq_ml(sq); oc[k] = seq_off(sq);
+          } else {
+            const int32_t bp = (int32_t)(uint32_t)sq;
+            const uint32_t stt = (uint32_t)(sq >> 32);
+            const uint32_t llc = L.stab[0][stt & 1023], mlc = L.stab[2][(stt >> 10) & 1023];
+            const uint32_t ofc = L.stab[1][stt >> 20] & 31;
+            uint32_t llbase, llb, mlbase, mlb;
+            ll_code(llc, &llbase, &llb);
+            ml_code(mlc, &mlbase, &mlb);
+            uint64_t tt = winu_top(winu_load(bsp, (uintptr_t)src, bp), 0);
+            const uint32_t ob = take_top(tt, ofc), mb = take_top(tt, mlb), lb = take_top(tt, llb);
+            oc[k] = (1u << ofc) + ob;             // offset_value for now
+            ml[k] = mlbase + mb;
+            ll[k] = llbase + lb;
+          }
+        }
+      }
+      // decode_offset (decoding_context.rs:50-75): this thread's map of the
+      // repeat offsets, scanned over the workgroup
+      uint32_t m[3];
+      rep_ident(m);
+#pragma unroll
+      for (int k = 0; k < K4F_KC; k++) (void)rep_step(m, oc[k], ll[k]);
+      k4f_scan_map(m, lane);
+#ifdef ZD_K4F_PROF
+      tp[np++] = __builtin_amdgcn_s_memtime();
+#endif
+      uint32_t ex[3];
+      ex[0] = (uint32_t)__shfl_up((int)m[0], 1, 64);
+      ex[1] = (uint32_t)__shfl_up((int)m[1], 1, 64);
+      ex[2] = (uint32_t)__shfl_up((int)m[2], 1, 64);
+      if (lane == 0) rep_ident(ex);
+      // lengths: this thread's sums, scanned the same way
+      uint32_t stot = 0, slit = 0;
+#pragma unroll
+      for (int k = 0; k < K4F_KC; k++) { stot += ll[k] + ml[k]; slit += ll[k]; }
+      uint32_t it = stot, il = slit;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a = (uint32_t)__shfl_up((int)it, d, 64), b = (uint32_t)__shfl_up((int)il, d, 64);
+        if (lane >= d) { it += a; il += b; }
+      }
+      if (lane == 63) {
+        L.wmap[wv][0] = m[0]; L.wmap[wv][1] = m[1]; L.wmap[wv][2] = m[2];
+        L.wsum[wv][0] = it; L.wsum[wv][1] = il;
+      }
+      if (t == 0) { L.err = ~0ull; L.lim = ~0ull; }
+      __syncthreads();
+      if (wv == 0) {                              // exclusive prefixes over the waves
+        uint32_t wm[3] = {OFF_SYM, OFF_SYM | (1u << 24), OFF_SYM | (2u << 24)};
+        uint32_t w0 = 0, w1 = 0;
+        if (lane < K4F_W) { wm[0] = L.wmap[lane][0]; wm[1] = L.wmap[lane][1]; wm[2] = L.wmap[lane][2];
+                            w0 = L.wsum[lane][0]; w1 = L.wsum[lane][1]; }
+        k4f_scan_map(wm, lane);
+        uint32_t i0 = w0, i1 = w1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t a = (uint32_t)__shfl_up((int)i0, d, 64), b = (uint32_t)__shfl_up((int)i1, d, 64);
+          if (lane >= d) { i0 += a; i1 += b; }
+        }
+        uint32_t pm[3];
+        pm[0] = (uint32_t)__shfl_up((int)wm[0], 1, 64);
+        pm[1] = (uint32_t)__shfl_up((int)wm[1], 1, 64);
+        pm[2] = (uint32_t)__shfl_up((int)wm[2], 1, 64);
+        if (lane == 0) rep_ident(pm);
+        if (lane == K4F_W - 1) { L.tot[0] = i0; L.tot[1] = i1; }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < K4F_W) {
+          L.wmap[lane][0] = pm[0]; L.wmap[lane][1] = pm[1]; L.wmap[lane][2] = pm[2];
+          L.wsum[lane][0] = i0 - w0; L.wsum[lane][1] = i1 - w1;
+        }
+      }
+      __syncthreads();
+      // the concrete state before this thread's sequences
+#ifdef ZD_K4F_PROF
+      tp[np++] = __builtin_amdgcn_s_memtime();
+#endif
+      uint32_t st3[3];
+      {
+        const uint32_t wp[3] = {L.wmap[wv][0], L.wmap[wv][1], L.wmap[wv][2]};
+        rc_compose(wp, ex);                       // ex: chunk input -> before this thread
+        const uint32_t in[3] = {rep_code(L.rep[rb][0]), rep_code(L.rep[rb][1]), rep_code(L.rep[rb][2])};
+        st3[0] = rc_apply(ex[0], in); st3[1] = rc_apply(ex[1], in); st3[2] = rc_apply(ex[2], in);
+      }
+#pragma unroll
+      for (int k = 0; k < K4F_KC; k++) oc[k] = rep_step(st3, oc[k], ll[k]);   // offset codes, concrete
+      const uint32_t pbase = pos + L.wsum[wv][0] + (it - stot);      // frame position of the first literal
+      const uint32_t lbase = lit_cursor + L.wsum[wv][1] + (il - slit);
+      const uint32_t ctot = L.tot[0], clit = L.tot[1];
+      if (cn - 1 >= b0 && cn - 1 < b0 + K4F_KC) {  // the chunk's last sequence: state out
+        L.rep[rb ^ 1][0] = rep_value(st3[0]); L.rep[rb ^ 1][1] = rep_value(st3[1]); L.rep[rb ^ 1][2] = rep_value(st3[2]);
+      }
+      // checks (decoding_context.rs:84-90, D9) in sequence order
+      {
+        uint32_t p = pbase, lp = lbase;
+        unsigned long long e = ~0ull, lim = ~0ull;
+#pragma unroll
+        for (int k = 0; k < K4F_KC; k++) {
+          if (b0 + k < cn) {
+            const uint32_t o = oc[k];
+            int code = 0;
+            if (o == OFF_NULL) code = ZD_E_NULL_OFFSET;
+            else if (o == OFF_UNDERFLOW) code = ZD_E_REF_PANIC;
+            else if ((uint64_t)lp + ll[k] > nl || (uint64_t)o > (uint64_t)p + ll[k]) code = ZD_E_IMPOSSIBLE_VALUE;
+            else if (ml[k] != 0 && o == 0) code = ZD_E_REF_PANIC;
+            const unsigned long long idx = c0 + b0 + k;
+            if (code && e == ~0ull) e = (idx << 8) | (uint32_t)(-code);
+            if ((uint64_t)p + ll[k] + ml[k] > cap && lim == ~0ull) lim = idx;
+          }
+          p += ll[k] + ml[k];
+          lp += ll[k];
+        }
+        if (e != ~0ull) atomicMin(&L.err, e);
+        if (lim != ~0ull) atomicMin(&L.lim, lim);
+      }
+      __syncthreads();
+      if (L.err != ~0ull || L.lim != ~0ull) {
+        if (L.err != ~0ull) err_key = make_key(PH_DECODE, j, DS_EXECUTE, (uint32_t)(L.err >> 8), -(int)(L.err & 0xFF));
+        else err_key = make_key(PH_LIMIT, j, DS_EXECUTE, (uint32_t)L.lim, ZD_E_OUT_OF_DOMAIN);
+        break;
+      }
+#ifdef ZD_K4F_PROF
+      tp[np++] = __builtin_amdgcn_s_memtime();
+#endif
+      // match bytes start unwritten; literal runs go in at once
+      {
+        uint32_t p = pbase, lp = lbase;
+#pragma unroll
+        for (int k = 0; k < K4F_KC; k++) {
+          if (ml[k]) k4f_bits_and(L.bits, p + ll[k], ml[k], false);
+          for (uint32_t x = 0; x < ll[k]; x += 16) {
+            const u32x4 v = lsrc ? ldg16(lsrc + lp + x) : f4;
+            sts_n((l_u8*)L.buf + p + x, v, ll[k] - x);
+          }
+          p += ll[k] + ml[k];
+          lp += ll[k];
+        }
+      }
+      __syncthreads();
+      // matches in rounds
+      uint32_t pend = 0;
+#ifdef ZD_K4F_PROF
+      tp[np++] = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+      for (int k = 0; k < K4F_KC; k++) pend |= (ml[k] != 0 ? 1u : 0u) << k;
+      // Parallel rounds while more matches wait than the ordered list holds
+      // (normally one round), then the rest in sequence order by one wave.
+      for (;;) {
+#ifdef ZD_K4F_PROF
+        rounds++;
+#endif
+        uint32_t q = pbase;
+#pragma unroll
+        for (int k = 0; k < K4F_KC; k++) {
+          q += ll[k];
+          if ((pend >> k) & 1) {
+            const uint32_t o = oc[k], mk = ml[k];
+            if (k4f_bits_all(L.bits, q - o, o < mk ? o : mk)) {
+              k4f_match((l_u8*)L.buf, q, o, mk);
+              __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the bytes land before their bits
+              k4f_bits_and(L.bits, q, mk, true);
+              pend &= ~(1u << k);
+            }
+          }
+          q += ml[k];
+        }
+        // ordered list slots: exclusive scan of the pending counts
+        const uint32_t c = (uint32_t)__popc(pend);
+        uint32_t ic = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)ic, d, 64);
+          if (lane >= d) ic += y;
+        }
+        if (lane == 63) L.wsum[wv][0] = ic;
+        __syncthreads();
+        uint32_t wb = 0, all = 0;
+        for (int w = 0; w < K4F_W; w++) {
+          const uint32_t x = L.wsum[w][0];
+          wb += w < wv ? x : 0;
+          all += x;
+        }
+        if (all <= K4F_LIST) {
+          uint32_t slot = wb + ic - c;
+          uint32_t q2 = pbase;
+#pragma unroll
+          for (int k = 0; k < K4F_KC; k++) {
+            q2 += ll[k];
+            if ((pend >> k) & 1) {
+              L.lq[slot] = q2; L.lo[slot] = oc[k]; L.lm[slot] = ml[k];
+              slot++;
+            }
+            q2 += ml[k];
+          }
+          __syncthreads();
+          if (wv == 0) k4f_ordered(L, all, lane);
+          break;
+        }
+        __syncthreads();
+      }
+      __syncthreads();
+      // every byte of the chunk is written now
+      {
+        const uint32_t w0 = pos >> 5, w1 = (pos + ctot + 31) >> 5;
+        for (uint32_t w = w0 + t; w < w1; w += K4F_T) L.bits[w] = ~0u;
+      }
+      pos += ctot;
+      lit_cursor += clit;
+#ifdef ZD_K4F_PROF
+      tp[np++] = __builtin_amdgcn_s_memtime();
+      if (t == 0 && blockIdx.x < 2)
+        printf("K4F wg %u chunk %u cn %u: dec %llu scan %llu chk %llu lit %llu match %llu rounds %d\n", blockIdx.x, c0, cn,
+               (unsigned long long)(tp[1] - tp[0]), (unsigned long long)(tp[2] - tp[1]), (unsigned long long)(tp[3] - tp[2]),
+               (unsigned long long)(tp[4] - tp[3]), (unsigned long long)(tp[5] - tp[4]), rounds);
+#endif
+      rb ^= 1;
+      __syncthreads();
+    }
+    if (err_key != KEY_NONE) break;
+    // leftover literals (decoding_context.rs:101-103)
+    if (lit_cursor < nl) {
+      const uint32_t rest = nl - lit_cursor;
+      if ((uint64_t)pos + rest > cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_OUT_OF_DOMAIN); break; }
+      for (uint32_t x = 16 * t; x < rest; x += 16 * K4F_T) {
+        const u32x4 v = lsrc ? ldg16(lsrc + lit_cursor + x) : f4;
+        sts_n((l_u8*)L.buf + pos + x, v, min(16u, rest - x));
+      }
+      pos += rest;
+    }
+    __syncthreads();
+  }
+  if (err_key != KEY_NONE) {
+    if (t == 0) key_min(fstate, f, err_key);
+    return;
+  }
+  // the frame -> HBM: aligned 16-byte stores, head and tail bytewise
+  uint8_t* out = outbase + F.out;
+  const uintptr_t oa = (uintptr_t)out;
+  const uint32_t head = (uint32_t)(((oa + 15) & ~(uintptr_t)15) - oa);
+  const uint32_t h = head < pos ? head : pos;
+  if ((uint32_t)t < h) out[t] = L.buf[t];
+  for (uint32_t x = h + 16 * t; x + 16 <= pos; x += 16 * K4F_T) *(g_u32x4*)(out + x) = lds16((const l_u8*)L.buf + x);
+  const uint32_t tail0 = pos > h ? h + ((pos - h) & ~15u) : pos;
+  if (tail0 + t < pos) out[tail0 + t] = L.buf[tail0 + t];
+  if (t == 0) {
+    S->out_len = pos;
+    S->rep[0] = L.rep[rb][0];
+    S->rep[1] = L.rep[rb][1];
+    S->rep[2] = L.rep[rb][2];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // compaction (frames without an exact FCS layout)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void zd_k_compact(const uint8_t* __restrict__ staging, uint8_t* dst,
@@ -1464,10 +1909,14 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses,
                        seqs);
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
-  if (a.n_frames && (a.kmask & 8))
+  if (a.n_frames > a.n_k4f && (a.kmask & 8))     // frames on the streaming K4 (the rest exit at once)
     hipLaunchKernelGGL(zd_k_execute, dim3(a.n_frames), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses);
+  if (a.n_k4f && (a.kmask & 8))
+    hipLaunchKernelGGL(zd_k_execute_lds, dim3(a.n_k4f), dim3(K4F_T), 0, s, a.src, a.out, frames, fstate, blocks, comp,
+                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
+                       (const uint16_t*)fses, (const uint32_t*)(ws + W.list_k4f));
   if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
   return hipGetLastError();
 }

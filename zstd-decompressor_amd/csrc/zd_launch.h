@@ -13,7 +13,7 @@ struct LaunchArgs {
   uint8_t* out;            // output base (d_dst or the plan's staging buffer)
   uint8_t* ws;             // workspace base
   Workspace W;
-  uint32_t n_tables, n_huf, n_seq, n_frames;
+  uint32_t n_tables, n_huf, n_seq, n_frames, n_k4f;
   hipStream_t stream;
   hipEvent_t* events;      // optional: 5 events recorded around the 4 kernels
   uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
@@ -27,6 +27,7 @@ hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* 
                           const uint64_t* d_to, const uint64_t* d_len, uint32_t n, hipStream_t s);
 
 constexpr int N_KERNELS = 4;
+constexpr uint32_t K4F_CAP = 128u << 10;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];
 
 }  // namespace zd
