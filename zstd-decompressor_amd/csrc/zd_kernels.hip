@@ -1022,6 +1022,7 @@ typedef __attribute__((address_space(3))) uint32_t l_u32a1 __attribute__((aligne
 typedef __attribute__((address_space(3))) uint16_t l_u16a1 __attribute__((aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4a1 g_cu32x4a1;
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(3))) u32x4 l_u32x4;
 
 __device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
 __device__ inline u32x4 ldg16_nt(const uint8_t* p) { return __builtin_nontemporal_load((g_cu32x4a1*)p); }
@@ -1040,11 +1041,15 @@ __device__ inline int64_t readlane_i64(int64_t x, int l) {
   int hi = __shfl((int)(uint32_t)((uint64_t)x >> 32), l, 64);
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
-__device__ inline uint32_t scan_incl_u32(uint32_t x, int lane) {
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
+// Inclusive prefix sum over the 64 lanes (all active) with DPP moves:
+// row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 and 31 across rows.
+__device__ inline uint32_t wave_scan_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
   return x;
 }
 
@@ -1193,6 +1198,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
+  __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];      // a batch's literal bytes
   const int lane = threadIdx.x;
   const uint32_t f = blockIdx.x;
   const FrameDesc F = frames[f];
@@ -1257,12 +1263,25 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       }
       __syncthreads();
     }
-    uint64_t nxt = lane < (int)n ? SQ[lane] : 0;
+    // Software pipeline over batches of 64 sequences: the records two
+    // batches ahead, the bitstream windows of the next batch and its literal
+    // bytes (1 KiB from the literal cursor, staged through LDS) one ahead,
+    // so a batch waits on nothing it issued itself.
+    const bool lit_stage = lsrc != nullptr;
+    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? SQ[i] : 0; };
+    auto win_of = [&](uint64_t r, bool v) -> WinU {
+      return winu_load(bsp, (uintptr_t)src, (v && !direct) ? (int32_t)(uint32_t)r : 0);
+    };
+    auto lit_of = [&](uint64_t cur) -> u32x4 {
+      return (lit_stage && cur + 16 * (uint64_t)lane < nl) ? ldg16(lsrc + cur + 16 * lane) : f4;
+    };
+    uint64_t recA = rec_at(lane), recB = rec_at(64 + lane);
+    WinU winA = win_of(recA, (uint32_t)lane < n);
+    u32x4 litA = lit_of(0);
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
       const uint32_t i = s0 + lane;
       const bool valid = i < n;
-      const uint64_t sq = nxt;
-      nxt = (i + 64 < n) ? SQ[i + 64] : 0;       // next batch's records, in flight
+      *(l_u32x4*)(stg + 16 * lane) = litA;       // this batch's literal bytes from the cursor on
       // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
       // K3 recorded the bit position and the three states; OF, ML, LL extra
       // bits are read here, in that order, below the position.
@@ -1270,26 +1289,28 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       bool giant = false;
       if (valid) {
         if (direct) {
-          ll = seq_ll(sq); ml = seq_ml(sq); ofv = seq_off(sq);
+          ll = seq_ll(recA); ml = seq_ml(recA); ofv = seq_off(recA);
           giant = ofv == DIRECT_GIANT;
         } else {
-          const int32_t pos = (int32_t)(uint32_t)sq;
-          const uint32_t stt = (uint32_t)(sq >> 32);
+          const uint32_t stt = (uint32_t)(recA >> 32);
           const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
           uint32_t llbase, llb, mlbase, mlb;
           ll_code(llc, &llbase, &llb);
           ml_code(mlc, &mlbase, &mlb);
-          uint64_t t = winu_top(winu_load(bsp, (uintptr_t)src, pos), 0);
+          uint64_t t = winu_top(winA, 0);
           const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
           ofv = (1u << ofc) + ob;
           ml = mlbase + mb;
           ll = llbase + lb;
         }
       }
+      // the next batch's windows, the records after it
+      const WinU winB = win_of(recB, s0 + 64 + lane < n);
+      const uint64_t recC = rec_at(s0 + 128 + lane);
       k4_room(X);
       const uint32_t tot = ll + ml;
-      const uint32_t inc_tot = scan_incl_u32(tot, lane);
-      const uint32_t inc_ll = scan_incl_u32(ll, lane);
+      const uint32_t inc_tot = wave_scan_incl(tot);
+      const uint32_t inc_ll = wave_scan_incl(ll);
       const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
       const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= X.space() - 16);
       const uint32_t k = (uint32_t)__popcll(fitm);
@@ -1337,7 +1358,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       const uint64_t badm = __ballot(dbad || imp || panic);
       if (badm) {
         const int b = __ffsll((long long)badm) - 1;
-        if ((uint32_t)b < (k ? k : 1u)) {
+        if (b < kk) {
           const int code = __shfl(dbad ? derr : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
           err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0 + b, code);
           break;
@@ -1345,8 +1366,9 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       }
       if (k == 0) {
         // one sequence larger than the window's room: the whole wave copies it
-        const uint32_t ll0 = __shfl(ll, 0, 64), ml0 = __shfl(ml, 0, 64);
-        const uint64_t off0 = (uint64_t)readlane_i64((int64_t)off, 0);
+        const uint32_t ll0 = (uint32_t)__builtin_amdgcn_readlane((int)ll, 0);
+        const uint32_t ml0 = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0);
+        const uint64_t off0 = readlane_u64(off, 0);
         if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, ll0) || !k4_emit_match(X, (l_u8*)pat, off0, ml0)) {
           err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN);
           break;
@@ -1354,19 +1376,26 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
         rep_push(val, 0 - prev, 1, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
         lit_cursor += ll0;
         s0 += 1;
-        if (s0 < n) nxt = (s0 + lane < n) ? SQ[s0 + lane] : 0;
+        recA = rec_at(s0 + lane); recB = rec_at(s0 + 64 + lane);
+        winA = win_of(recA, s0 + lane < n);
+        litA = lit_of(lit_cursor);
         continue;
       }
-      const uint32_t T = __shfl(inc_tot, k - 1, 64);
-      const uint32_t L = __shfl(inc_ll, k - 1, 64);
+      const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
+      const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
       if (X.pos + (int64_t)T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN); break; }
+      // the next batch's literal bytes
+      const u32x4 litB = lit_of(lit_cursor + L);
       const bool act = (uint32_t)lane < k;
-      // literals (every lane its own run)
+      __syncthreads();                                 // staged literals visible
+      // literals (every lane its own run; from the stage when it holds them)
       if (act && ll) {
         l_u8* d = X.at(X.pos + opos);
-        for (uint32_t x = 0; x < ll; x += 16) {
-          const u32x4 v = lsrc ? ldg16(lsrc + lit_cursor + lpos + x) : f4;
-          sts_n(d + x, v, ll - x);
+        if (!lit_stage || lpos + ll <= 1024) {
+          const l_u8* sp = (const l_u8*)stg + lpos;
+          for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
+        } else {
+          for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
         }
       }
       // matches, in frontier rounds
@@ -1402,7 +1431,13 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
       lit_cursor += L;
       X.pos += T;
       s0 += k;
-      if (k < 64 && s0 < n) nxt = (s0 + lane < n) ? SQ[s0 + lane] : 0;
+      if (k == 64) {
+        recA = recB; winA = winB; recB = recC; litA = litB;
+      } else if (s0 < n) {                             // a partial batch: the pipeline restarts at s0
+        recA = rec_at(s0 + lane); recB = rec_at(s0 + 64 + lane);
+        winA = win_of(recA, s0 + lane < n);
+        litA = lit_of(lit_cursor);
+      }
       k4_flush(X, false);
     }
     if (err_key != KEY_NONE) break;
