@@ -1010,9 +1010,18 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
 // source period by period, byte q+j = byte q-off+(j mod off), which is the
 // reference's byte-by-byte push (decoding_context.rs:95-98).
 // ---------------------------------------------------------------------------
-constexpr int K4_W = 4096;                    // history kept after a slide
-constexpr int K4_B = 4096;                    // room for a batch
-constexpr int K4_C = K4_W + K4_B + 32;        // window bytes
+#ifndef ZD_K4_W
+#define ZD_K4_W 2048
+#endif
+#ifndef ZD_K4_B
+#define ZD_K4_B 2048
+#endif
+constexpr int K4_W = ZD_K4_W;                 // history kept after a slide
+constexpr int K4_B = ZD_K4_B;                 // room kept for a batch (a slide when less is left)
+#ifndef ZD_K4_C
+#define ZD_K4_C (8192 + 32)
+#endif
+constexpr int K4_C = ZD_K4_C;                 // window bytes
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4a1 __attribute__((ext_vector_type(4), aligned(1)));
 typedef __attribute__((address_space(3))) uint8_t l_u8;
@@ -1187,7 +1196,10 @@ __device__ bool k4_emit_match(K4& X, l_u8* pat, uint64_t off, uint64_t n) {
   return true;
 }
 
-__global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ src, uint8_t* outbase,
+#ifndef ZD_K4_MINW
+#define ZD_K4_MINW 1
+#endif
+__global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __restrict__ src, uint8_t* outbase,
                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
                                                    const BlockRec* __restrict__ blocks,
                                                    const CompBlock* __restrict__ comp,
@@ -1225,6 +1237,15 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
   }
   uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
   uint64_t err_key = KEY_NONE;
+  // HBM holds [0, fl_safe) with every store completed (the bytes two batches
+  // back); fl_last = the flush boundary after the previous batch
+  int64_t fl_safe = X.fl, fl_last = X.fl;
+#ifdef ZD_K4_PROF
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime(), nb = 0, nr = 0;
+#define K4P(i) do { const uint64_t tn = __builtin_amdgcn_s_memtime(); ph[i] += tn - tq; tq = tn; } while (0)
+#else
+#define K4P(i) do { } while (0)
+#endif
 
   for (uint32_t j = 0; j < F.nblocks && err_key == KEY_NONE; j++) {
     const BlockRec B = blocks[F.first_block + j];
@@ -1281,6 +1302,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
       const uint32_t i = s0 + lane;
       const bool valid = i < n;
+      K4P(7);
       *(l_u32x4*)(stg + 16 * lane) = litA;       // this batch's literal bytes from the cursor on
       // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
       // K3 recorded the bit position and the three states; OF, ML, LL extra
@@ -1304,6 +1326,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
           ll = llbase + lb;
         }
       }
+      K4P(0);
       // the next batch's windows, the records after it
       const WinU winB = win_of(recB, s0 + 64 + lane < n);
       const uint64_t recC = rec_at(s0 + 128 + lane);
@@ -1349,6 +1372,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
         prev = ri;
         if (e) break;                                  // the frame stops at this sequence
       }
+      K4P(1);
       // checks (decoding_context.rs:86-90, D9)
       const uint64_t before = (uint64_t)X.pos + opos;
       const bool dbad = valid && derr != 0;
@@ -1398,13 +1422,27 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
           for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
         }
       }
-      // matches, in frontier rounds
+      K4P(2);
+      // matches whose source lies wholly in HBM, flushed two batches ago or
+      // earlier (those stores completed before this batch's waits), copy at
+      // once; the rest in frontier rounds
       const int64_t q = X.pos + opos + ll;
       const int64_t slo = q - (int64_t)off;
       const int64_t shi = slo + (int64_t)(off < ml ? off : ml);
-      if (__ballot(act && ml && slo < X.hs)) wait_vm();
-      uint64_t done = __ballot(!act || ml == 0);
+      const bool far = act && ml && off >= 16 && shi <= (X.hs < fl_safe ? X.hs : fl_safe);
+      if (far) {                                       // ml < off here: no overlap
+        const uint8_t* sp = X.out + slo;
+        const u32x4 v0 = ldg16_nt(sp);
+        const u32x4 v1 = ml > 16 ? ldg16_nt(sp + 16) : v0;
+        l_u8* d = X.at(q);
+        sts_n(d, v0, ml);
+        if (ml > 16) sts_n(d + 16, v1, ml - 16);
+        for (uint32_t x = 32; x < ml; x += 16) sts_n(d + x, ldg16_nt(sp + x), ml - x);
+      }
+      if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
+      uint64_t done = __ballot(!act || ml == 0 || far);
       __syncthreads();
+      K4P(3);
       while (done != ~0ull) {
         const int U = __ffsll((long long)~done) - 1;
         const int64_t qU = readlane_i64(q, U);
@@ -1426,11 +1464,20 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
         }
         done |= __ballot(mine);
         __syncthreads();
+#ifdef ZD_K4_PROF
+        nr++;
+#endif
       }
+      K4P(4);
+#ifdef ZD_K4_PROF
+      nb++;
+#endif
       rep_push(val, (int)k - 1 - prev, (int)k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);   // state after lane k - 1
       lit_cursor += L;
       X.pos += T;
       s0 += k;
+      fl_safe = fl_last;
+      fl_last = X.fl;
       if (k == 64) {
         recA = recB; winA = winB; recB = recC; litA = litB;
       } else if (s0 < n) {                             // a partial batch: the pipeline restarts at s0
@@ -1439,6 +1486,7 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
         litA = lit_of(lit_cursor);
       }
       k4_flush(X, false);
+      K4P(5);
     }
     if (err_key != KEY_NONE) break;
     // leftover literals (decoding_context.rs:101-103)
@@ -1450,6 +1498,13 @@ __global__ __launch_bounds__(64) void zd_k_execute(const uint8_t* __restrict__ s
     return;
   }
   k4_flush(X, true);
+#ifdef ZD_K4_PROF
+  if (lane == 0 && f < 3)
+    printf("K4 frame %u batches %llu rounds %llu: rec/val %llu scan/rep %llu chk/lit %llu far %llu rounds %llu flush %llu top %llu\n", f,
+           (unsigned long long)nb, (unsigned long long)nr, (unsigned long long)ph[0], (unsigned long long)ph[1],
+           (unsigned long long)ph[2], (unsigned long long)ph[3], (unsigned long long)ph[4], (unsigned long long)ph[5],
+           (unsigned long long)ph[7]);
+#endif
   if (lane == 0) {
     S->out_len = (uint64_t)X.pos;
     S->rep[0] = rep[0];
