@@ -524,7 +524,7 @@ typedef __attribute__((address_space(1))) uint64_t g_u64a1 __attribute__((aligne
 // absent tree node) goes symbol by symbol with the reference's checks.
 template <typename LP>
 __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP lut, int p, uint8_t* out,
-                          uint32_t cap, uint32_t* count_out) {
+                          uint32_t cap, uint32_t* count_out, uint8_t* dummy) {
   uint32_t count = 0;
   *count_out = 0;
   if (size == 0) return ZD_E_EMPTY_INPUT_DATA;
@@ -532,8 +532,14 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
   const uint32_t sh = 64 - p;
+  // The next group's window is loaded before this group's store: vmcnt
+  // drains in issue order, so a group waits for its window, not the store.
+  // The loop entry repeats that order (a store into the block's literal
+  // slack, never read) so the wait at the loop head stays vmcnt(1).
+  WinU w = winu_load(bs, base, pos);
+  asm volatile("" ::: "memory");
+  *(g_u64a1*)dummy = 0;
   while (pos >= K2_GROUP * LUT_MAX_BITS && count + K2_GROUP <= cap) {
-    const WinU w = winu_load(bs, base, pos);
     uint64_t acc = 0;
     uint32_t used = 0, bad = 0;
 #pragma unroll
@@ -550,9 +556,11 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
       }
     }
     if (bad) break;                            // redo this group with the exact checks
+    pos -= (int32_t)used;
+    w = winu_load(bs, base, pos);
+    asm volatile("" ::: "memory");
     *(g_u64a1*)(out + count) = acc;
     count += K2_GROUP;
-    pos -= (int32_t)used;
   }
   int st = 0;
   while (pos > 0 && !st) {
@@ -622,13 +630,15 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint32_t cap = k < m - 1 ? seg : (R > start ? R - start : 0);
     const uint8_t* blk = src + C.src;
     const uintptr_t lo = (uintptr_t)src;
+    uint8_t* slack = lits + C.lit_out + R + 8;       // the block's literal slot has 16 bytes past R
     uint32_t count;
     int st;
     if (use_lds)
       st = huf_stream<const lds_u16*>(blk + off, C.stream_size[k], lo, (const lds_u16*)lut[b], p,
-                                      lits + C.lit_out + start, cap, &count);
+                                      lits + C.lit_out + start, cap, &count, slack);
     else
-      st = huf_stream<g_u16*>(blk + off, C.stream_size[k], lo, (g_u16*)g, p, lits + C.lit_out + start, cap, &count);
+      st = huf_stream<g_u16*>(blk + off, C.stream_size[k], lo, (g_u16*)g, p, lits + C.lit_out + start, cap, &count,
+                              slack);
     counts[b][k] = count;
     errs[b][k] = st;
     if (st) key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, k, st));
@@ -666,10 +676,11 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint32_t at = redo_at[b][k];
     if (use_lds)
       (void)huf_stream<const lds_u16*>(blk + off, C.stream_size[k], (uintptr_t)src,
-                                       (const lds_u16*)lut[b], p, lits + C.lit_out + at, counts[b][k], &count);
+                                       (const lds_u16*)lut[b], p, lits + C.lit_out + at, counts[b][k], &count,
+                                       lits + C.lit_out + R + 8);
     else
       (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)src, (g_u16*)g, p,
-                               lits + C.lit_out + at, counts[b][k], &count);
+                               lits + C.lit_out + at, counts[b][k], &count, lits + C.lit_out + R + 8);
   }
 }
 
