@@ -90,6 +90,20 @@ def cpu_baseline(frame_set: bytes, threads: int, budget_s: float = 20.0):
                       f"oracle/zd_oracle.c on {threads} host threads, {dt:.1f} s"}
 
 
+def traffic_of(kernel: str, args):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE + WRITE_SIZE, rocprofv3
+    --pmc passes of scripts/full_run.sh on the default workload, kept in
+    profiles/traffic.json); None for other workloads or when absent."""
+    if (args.workload, args.unique_mib, args.replicas) != ("c4", 1024, 10):
+        return None
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        k = json.load(open(path))["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if not k else round(k["traffic"] / 1e9, 3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -255,7 +269,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic_of(dom, args),
+                "traffic_unit": "GB per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, profiles/traffic.json)",
+                "alg_bytes_per_launch": int(alg_per_launch),
                 "pipeline_achieved": round(alg_per_launch / (ms_per_step / 1e3) / 1e9, 1),
                 "pipeline_frac": round(alg_per_launch / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             },
