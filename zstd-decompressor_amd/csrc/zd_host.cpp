@@ -673,6 +673,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
+  if (const char* g = getenv("ZD_K4_GRID")) a.k4_grid = (uint32_t)strtoul(g, nullptr, 0);
   HIPCHK(launch_pipeline(a));
   P->launched = true;
   return ZD_OK;

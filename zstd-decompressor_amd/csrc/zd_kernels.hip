@@ -1217,18 +1217,20 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                                                    const CompState* __restrict__ cstate,
                                                    const uint8_t* __restrict__ lits,
                                                    const uint64_t* __restrict__ seqs,
-                                                   const uint16_t* __restrict__ fses) {
+                                                   const uint16_t* __restrict__ fses, uint32_t n_frames) {
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
   __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];      // a batch's literal bytes
   const int lane = threadIdx.x;
-  const uint32_t f = blockIdx.x;
+  // persistent over frames when the grid is capped (frames in flight sized
+  // to keep their outputs cache-resident)
+  for (uint32_t f = blockIdx.x; f < n_frames; f += gridDim.x) {
   const FrameDesc F = frames[f];
-  if (F.lds) return;                             // K4F executes this frame
+  if (F.lds) continue;                           // K4F executes this frame
   FrameState* S = &fstate[f];
   const uint64_t key0 = S->key;
-  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
+  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) continue;
 
   K4 X;
   X.buf = (l_u8*)win;
@@ -1506,7 +1508,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   }
   if (err_key != KEY_NONE) {
     if (lane == 0) key_min(fstate, f, err_key);
-    return;
+    continue;
   }
   k4_flush(X, true);
 #ifdef ZD_K4_PROF
@@ -1521,6 +1523,8 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     S->rep[0] = rep[0];
     S->rep[1] = rep[1];
     S->rep[2] = rep[2];
+  }
+  __syncthreads();                               // the window is reused by the next frame
   }
 }
 
@@ -2011,9 +2015,9 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        seqs);
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   if (a.n_frames > a.n_k4f && (a.kmask & 8))     // frames on the streaming K4 (the rest exit at once)
-    hipLaunchKernelGGL(zd_k_execute, dim3(a.n_frames), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
-                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
-                       (const uint16_t*)fses);
+    hipLaunchKernelGGL(zd_k_execute, dim3(a.k4_grid && a.k4_grid < a.n_frames ? a.k4_grid : a.n_frames), dim3(64), 0,
+                       s, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
+                       (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, a.n_frames);
   if (a.n_k4f && (a.kmask & 8))
     hipLaunchKernelGGL(zd_k_execute_lds, dim3(a.n_k4f), dim3(K4F_T), 0, s, a.src, a.out, frames, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,

@@ -17,6 +17,7 @@ struct LaunchArgs {
   hipStream_t stream;
   hipEvent_t* events;      // optional: 5 events recorded around the 4 kernels
   uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
+  uint32_t k4_grid = 0;    // cap on K4 workgroups (persistent over frames); 0 = one per frame
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
