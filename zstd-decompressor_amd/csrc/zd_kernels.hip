@@ -1063,15 +1063,6 @@ __device__ inline int64_t readlane_i64(int64_t x, int l) {
 }
 // Inclusive prefix sum over the 64 lanes (all active) with DPP moves:
 // row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 and 31 across rows.
-__device__ inline uint32_t wave_scan_incl(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-  return x;
-}
 
 __device__ inline uint64_t readlane_u64(uint64_t x, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
@@ -1089,50 +1080,52 @@ __device__ inline void rep_push(uint64_t val, int cnt, int end, uint64_t r0, uin
   *a0 = b0; *a1 = b1; *a2 = b2;
 }
 
+// Frame positions are 32-bit: frames with sequences stay below MAX_FRAME_OUT
+// (2^27) and the planner caps every frame the streaming K4 runs below 2^31.
 struct K4 {
   l_u8* buf;
   uint8_t* out;            // frame output (frame position 0)
-  intptr_t oabs;
-  int64_t hs;              // frame position of buf[0]; (oabs + hs) % 16 == 0
-  int64_t pos;             // decoded length
-  int64_t fl;              // HBM holds [0, fl)
-  int64_t cap;
+  int32_t a0;              // frame position of the first 16-byte aligned HBM address (0..15)
+  int32_t hs;              // frame position of buf[0]; hs = a0 (mod 16), may be < 0
+  int32_t pos;             // decoded length
+  int32_t fl;              // HBM holds [0, fl)
+  int32_t cap;
   int lane;
-  __device__ inline l_u8* at(int64_t p) const { return buf + (p - hs); }
-  __device__ inline int64_t space() const { return K4_C - (pos - hs); }
+  __device__ inline l_u8* at(int32_t p) const { return buf + (p - hs); }
+  __device__ inline int32_t space() const { return K4_C - (pos - hs); }
+  __device__ inline int32_t alignd(int32_t p) const { return ((p - a0) & ~15) + a0; }
   // 16 bytes of frame output at p (p >= 0): LDS when inside the window, else HBM
-  __device__ inline u32x4 src16(int64_t p) const { return p >= hs ? lds16(at(p)) : ldg16_nt(out + p); }
+  __device__ inline u32x4 src16(int32_t p) const { return p >= hs ? lds16(at(p)) : ldg16_nt(out + p); }
 };
 
 // HBM <- window: the aligned 16-byte chunks of [fl, pos) (all of it if final)
 __device__ void k4_flush(K4& X, bool final) {
-  const intptr_t A = (X.oabs + X.fl) & ~(intptr_t)15, E = (X.oabs + X.pos) & ~(intptr_t)15;
-  for (intptr_t c = A + 16 * X.lane; c < E; c += 1024) {
-    const u32x4 v = lds16(X.at(c - X.oabs));
-    if (c >= X.oabs) {
-      *(g_u32x4*)c = v;
+  const int32_t A = X.alignd(X.fl), E = X.alignd(X.pos);
+  for (int32_t c = A + 16 * X.lane; c < E; c += 1024) {
+    const u32x4 v = lds16(X.at(c));
+    if (c >= 0) {
+      *(g_u32x4*)(X.out + c) = v;
     } else {                                   // the frame's head chunk: only its own bytes
-      for (intptr_t b = X.oabs; b < c + 16; b++) *(uint8_t*)b = *X.at(b - X.oabs);
+      for (int32_t b = 0; b < c + 16; b++) X.out[b] = *X.at(b);
     }
   }
   if (final) {
-    const intptr_t lo = E > X.oabs + X.fl ? E : X.oabs + X.fl;
-    for (intptr_t b = lo + X.lane; b < X.oabs + X.pos; b += 64) *(uint8_t*)b = *X.at(b - X.oabs);
+    for (int32_t b = (E > X.fl ? E : X.fl) + X.lane; b < X.pos; b += 64) X.out[b] = *X.at(b);
     X.fl = X.pos;
-  } else if (E - X.oabs > X.fl) {
-    X.fl = E - X.oabs;
+  } else if (E > X.fl) {
+    X.fl = E;
   }
 }
 
-// Slides the window so that at least K4_B - 16 bytes are free (keeps K4_W of
+// Slides the window so that at least K4_B bytes are free (keeps K4_W of
 // history).  An ascending chunked copy: each 1 KiB step reads all its chunks
 // before writing any, and later steps read above everything written so far.
 __device__ void k4_room(K4& X) {
   if (X.space() >= K4_B) return;
-  const int64_t nh = ((X.oabs + X.pos - K4_W) & ~(intptr_t)15) - X.oabs;   // <= fl: pos - fl < 16
-  const int64_t n = X.pos - nh;                // <= K4_W + 15 bytes move down by nh - hs
+  const int32_t nh = X.alignd(X.pos - K4_W);   // <= fl: pos - fl < 16
+  const int32_t n = X.pos - nh;                // <= K4_W + 15 bytes move down by nh - hs
   const l_u8* from = X.at(nh);
-  for (int64_t x = 16 * X.lane; x - 16 * X.lane < n; x += 1024) {
+  for (int32_t x = 16 * X.lane; x - 16 * X.lane < n; x += 1024) {
     u32x4 v;
     if (x < n) v = lds16(from + x);
     __builtin_amdgcn_wave_barrier();
@@ -1145,20 +1138,20 @@ __device__ void k4_room(K4& X) {
 
 // Appends n literal bytes from s (HBM) or the fill byte (s == nullptr), the
 // whole wave copying 16 bytes per lane.  false: past the frame capacity.
-__device__ bool k4_emit_lits(K4& X, const uint8_t* s, uint32_t fill, uint64_t n) {
+__device__ bool k4_emit_lits(K4& X, const uint8_t* s, uint32_t fill, uint32_t n) {
   const u32x4 f4 = (u32x4){fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u};
   while (n) {
     k4_room(X);
-    const int64_t chunk = (int64_t)n < X.space() - 16 ? (int64_t)n : X.space() - 16;
-    if (X.pos + chunk > X.cap) return false;
-    for (int64_t x = 16 * X.lane; x < chunk; x += 1024) {
+    const int32_t chunk = (int32_t)min(n, (uint32_t)(X.space() - 16));
+    if ((int64_t)X.pos + chunk > X.cap) return false;
+    for (int32_t x = 16 * X.lane; x < chunk; x += 1024) {
       const u32x4 v = s ? ldg16(s + x) : f4;
       sts_n(X.at(X.pos + x), v, (uint32_t)(chunk - x));
     }
     __syncthreads();
     X.pos += chunk;
     if (s) s += chunk;
-    n -= (uint64_t)chunk;
+    n -= (uint32_t)chunk;
     k4_flush(X, false);
   }
   return true;
@@ -1169,42 +1162,53 @@ __device__ bool k4_emit_lits(K4& X, const uint8_t* s, uint32_t fill, uint64_t n)
 // start q, in the window or (once slid out) in HBM.  A period shorter than 16
 // is first unrolled into `pat` (48 bytes of it), so every 16-byte piece is one
 // LDS read.
-__device__ bool k4_emit_match(K4& X, l_u8* pat, uint64_t off, uint64_t n) {
-  const int64_t q = X.pos;                     // match start
-  uint64_t j0 = 0;
+__device__ bool k4_emit_match(K4& X, l_u8* pat, uint32_t off, uint32_t n) {
+  const int32_t q = X.pos;                     // match start
+  uint32_t j0 = 0;
   const bool small = off < 16;
-  const bool need_hbm = !small && (int64_t)(q - (int64_t)off) < X.hs;
+  const bool need_hbm = !small && q - (int32_t)off < X.hs;
   if (small) {                                 // q - off >= hs here: the period is in the window
-    if (X.lane < 48) pat[X.lane] = *X.at(q - (int64_t)off + (int64_t)((uint64_t)X.lane % off));
+    if (X.lane < 48) pat[X.lane] = *X.at(q - (int32_t)off + (int32_t)((uint32_t)X.lane % off));
     __syncthreads();
   }
   if (__ballot(need_hbm)) wait_vm();
   while (j0 < n) {
     k4_room(X);
     if (j0 && !small) wait_vm();              // the last chunk's flush, before reading it back
-    const int64_t chunk = (int64_t)(n - j0) < X.space() - 16 ? (int64_t)(n - j0) : X.space() - 16;
-    if (X.pos + chunk > X.cap) return false;
-    for (int64_t x = 16 * X.lane; x < chunk; x += 1024) {
-      const uint64_t j = j0 + (uint64_t)x, r = j % off;
+    const int32_t chunk = (int32_t)min(n - j0, (uint32_t)(X.space() - 16));
+    if ((int64_t)X.pos + chunk > X.cap) return false;
+    for (int32_t x = 16 * X.lane; x < chunk; x += 1024) {
+      const uint32_t j = j0 + (uint32_t)x, r = j % off;
       const uint32_t m = (uint32_t)(chunk - x < 16 ? chunk - x : 16);
       if (small) {
         sts_n(X.at(X.pos + x), lds16(pat + r), m);
       } else if (r + m <= off) {
-        sts_n(X.at(X.pos + x), X.src16(q - (int64_t)off + (int64_t)r), m);
+        sts_n(X.at(X.pos + x), X.src16(q - (int32_t)off + (int32_t)r), m);
       } else {                                 // the piece wraps at the period
         for (uint32_t b = 0; b < m; b++) {
-          const uint64_t rb = (j + b) % off;
-          const int64_t p = q - (int64_t)off + (int64_t)rb;
+          const int32_t p = q - (int32_t)off + (int32_t)((j + b) % off);
           *X.at(X.pos + x + b) = p >= X.hs ? *X.at(p) : __builtin_nontemporal_load(X.out + p);
         }
       }
     }
     __syncthreads();
     X.pos += chunk;
-    j0 += (uint64_t)chunk;
+    j0 += (uint32_t)chunk;
     k4_flush(X, false);
   }
   return true;
+}
+
+// Inclusive prefix sum over the 64 lanes (all active) with DPP moves:
+// row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 and 31 across rows.
+__device__ inline uint32_t wave_scan_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
 }
 
 #ifndef ZD_K4_MINW
@@ -1223,8 +1227,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
   __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];      // a batch's literal bytes
   const int lane = threadIdx.x;
-  // persistent over frames when the grid is capped (frames in flight sized
-  // to keep their outputs cache-resident)
+  // persistent over frames when the grid is capped
   for (uint32_t f = blockIdx.x; f < n_frames; f += gridDim.x) {
   const FrameDesc F = frames[f];
   if (F.lds) continue;                           // K4F executes this frame
@@ -1235,24 +1238,23 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   K4 X;
   X.buf = (l_u8*)win;
   X.out = outbase + F.out;
-  X.oabs = (intptr_t)X.out;
+  X.a0 = (int32_t)((16 - ((uintptr_t)X.out & 15)) & 15);
   X.lane = lane;
-  X.pos = (int64_t)F.out_len0;
+  X.pos = (int32_t)F.out_len0;
   X.fl = X.pos;
-  X.cap = (int64_t)F.out_cap;
+  X.cap = (int32_t)(F.out_cap < 0x7FFFFFF0ull ? F.out_cap : 0x7FFFFFF0ull);
   {
     // window start: aligned, at most K4_W bytes back (context API: the
     // existing output's tail comes back from HBM)
-    const int64_t back = X.pos > K4_W ? X.pos - K4_W : 0;
-    X.hs = ((X.oabs + back) & ~(intptr_t)15) - X.oabs;
-    for (int64_t p = (X.hs > 0 ? X.hs : 0) + lane; p < X.pos; p += 64) *X.at(p) = X.out[p];
+    X.hs = X.alignd(X.pos > K4_W ? X.pos - K4_W : 0);
+    for (int32_t p = (X.hs > 0 ? X.hs : 0) + lane; p < X.pos; p += 64) *X.at(p) = X.out[p];
     __syncthreads();
   }
   uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
   uint64_t err_key = KEY_NONE;
   // HBM holds [0, fl_safe) with every store completed (the bytes two batches
   // back); fl_last = the flush boundary after the previous batch
-  int64_t fl_safe = X.fl, fl_last = X.fl;
+  int32_t fl_safe = X.fl, fl_last = X.fl;
 #ifdef ZD_K4_PROF
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime(), nb = 0, nr = 0;
 #define K4P(i) do { const uint64_t tn = __builtin_amdgcn_s_memtime(); ph[i] += tn - tq; tq = tn; } while (0)
@@ -1277,12 +1279,12 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     if (CS.stop) break;
     const uint8_t* lsrc = nullptr;
     uint32_t lfill = 0;
-    uint64_t nl;
+    uint32_t nl;
     if (C.lit_type == LIT_RAW) { lsrc = src + C.src + C.lit_data; nl = C.lit_regen; }
     else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle; nl = C.lit_regen; }
     else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
     const u32x4 f4 = (u32x4){lfill * 0x01010101u, lfill * 0x01010101u, lfill * 0x01010101u, lfill * 0x01010101u};
-    uint64_t lit_cursor = 0;
+    uint32_t lit_cursor = 0;
     const uint64_t* SQ = seqs + C.seq_out;
     const uint32_t n = C.nseq;
     const bool direct = C.seq_direct != 0;
@@ -1300,206 +1302,209 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     // Software pipeline over batches of 64 sequences: the records two
     // batches ahead, the bitstream windows of the next batch and its literal
     // bytes (1 KiB from the literal cursor, staged through LDS) one ahead,
-    // so a batch waits on nothing it issued itself.
+    // so a batch waits on nothing it issued itself.  A sequence too large
+    // for the window's room leaves the batch loop; the whole wave copies it
+    // and the pipeline restarts after it.
     const bool lit_stage = lsrc != nullptr;
     auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? SQ[i] : 0; };
     auto win_of = [&](uint64_t r, bool v) -> WinU {
       return winu_load(bsp, (uintptr_t)src, (v && !direct) ? (int32_t)(uint32_t)r : 0);
     };
-    auto lit_of = [&](uint64_t cur) -> u32x4 {
-      return (lit_stage && cur + 16 * (uint64_t)lane < nl) ? ldg16(lsrc + cur + 16 * lane) : f4;
+    auto lit_of = [&](uint32_t cur) -> u32x4 {
+      return (lit_stage && cur + 16 * (uint32_t)lane < nl) ? ldg16(lsrc + cur + 16 * lane) : f4;
     };
-    uint64_t recA = rec_at(lane), recB = rec_at(64 + lane);
-    WinU winA = win_of(recA, (uint32_t)lane < n);
-    u32x4 litA = lit_of(0);
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
-      const uint32_t i = s0 + lane;
-      const bool valid = i < n;
-      K4P(7);
-      *(l_u32x4*)(stg + 16 * lane) = litA;       // this batch's literal bytes from the cursor on
-      // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
-      // K3 recorded the bit position and the three states; OF, ML, LL extra
-      // bits are read here, in that order, below the position.
-      uint32_t ll = 0, ml = 0, ofv = 0;
-      bool giant = false;
-      if (valid) {
-        if (direct) {
-          ll = seq_ll(recA); ml = seq_ml(recA); ofv = seq_off(recA);
-          giant = ofv == DIRECT_GIANT;
-        } else {
-          const uint32_t stt = (uint32_t)(recA >> 32);
-          const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
-          uint32_t llbase, llb, mlbase, mlb;
-          ll_code(llc, &llbase, &llb);
-          ml_code(mlc, &mlbase, &mlb);
-          uint64_t t = winu_top(winA, 0);
-          const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
-          ofv = (1u << ofc) + ob;
-          ml = mlbase + mb;
-          ll = llbase + lb;
+      uint64_t recA = rec_at(s0 + lane), recB = rec_at(s0 + 64 + lane);
+      WinU winA = win_of(recA, s0 + lane < n);
+      u32x4 litA = lit_of(lit_cursor);
+      bool big = false;                              // batch loop left for one large sequence
+      uint32_t bll = 0, bml = 0;
+      uint64_t boff = 0;
+      for (;;) {
+        const uint32_t i = s0 + lane;
+        const bool valid = i < n;
+        K4P(7);
+        *(l_u32x4*)(stg + 16 * lane) = litA;         // this batch's literal bytes from the cursor on
+        // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
+        // K3 recorded the bit position and the three states; OF, ML, LL
+        // extra bits are read here, in that order, below the position.
+        uint32_t ll = 0, ml = 0, ofv = 0;
+        bool giant = false;
+        if (valid) {
+          if (direct) {
+            ll = seq_ll(recA); ml = seq_ml(recA); ofv = seq_off(recA);
+            giant = ofv == DIRECT_GIANT;
+          } else {
+            const uint32_t stt = (uint32_t)(recA >> 32);
+            const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
+            uint32_t llbase, llb, mlbase, mlb;
+            ll_code(llc, &llbase, &llb);
+            ml_code(mlc, &mlbase, &mlb);
+            uint64_t t = winu_top(winA, 0);
+            const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
+            ofv = (1u << ofc) + ob;
+            ml = mlbase + mb;
+            ll = llbase + lb;
+          }
         }
-      }
-      K4P(0);
-      // the next batch's windows, the records after it
-      const WinU winB = win_of(recB, s0 + 64 + lane < n);
-      const uint64_t recC = rec_at(s0 + 128 + lane);
-      k4_room(X);
-      const uint32_t tot = ll + ml;
-      const uint32_t inc_tot = wave_scan_incl(tot);
-      const uint32_t inc_ll = wave_scan_incl(ll);
-      const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
-      const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= X.space() - 16);
-      const uint32_t k = (uint32_t)__popcll(fitm);
-      const int kk = k ? (int)k : 1;                   // lanes this batch executes
-      // decode_offset (decoding_context.rs:50-75): fresh offsets (> 3) are
-      // direct; the rare repeat codes walk the batch in order on the scalar
-      // unit, each from the state the fresh offsets before it left.
-      const bool fresh = ofv > 3;
-      const uint64_t val = giant ? OFF_HUGE : (uint64_t)ofv - 3;
-      uint64_t off = val;
-      int derr = 0;
-      uint64_t rm = __ballot(valid && !fresh && lane < kk);
-      uint64_t r0 = rep[0], r1 = rep[1], r2 = rep[2];   // state after lane `prev`
-      int prev = -1;
-      while (rm) {
-        const int ri = __ffsll((long long)rm) - 1;
-        rm &= rm - 1;
-        uint64_t a0, a1, a2;
-        rep_push(val, ri - prev - 1, ri, r0, r1, r2, &a0, &a1, &a2);
-        const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)ofv, ri);
-        const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)ll, ri);
-        uint64_t o = 0;
-        int e = 0;
-        if (oi == 0) {
-          e = ZD_E_NULL_OFFSET;
-        } else {
-          const uint32_t idx = oi - (li != 0 ? 1u : 0u);
-          if (idx == 0) { o = a0; }
-          else if (idx == 1) { o = a1; a1 = a0; a0 = o; }
-          else if (idx == 2) { o = a2; a2 = a1; a1 = a0; a0 = o; }
-          else if (a0 == 0) { e = ZD_E_REF_PANIC; }     // usize underflow of offsets[0] -= 1
-          else { o = a0 - 1; a2 = a1; a1 = a0; a0 = o; }
+        K4P(0);
+        // the next batch's windows, the records after it
+        const WinU winB = win_of(recB, s0 + 64 + lane < n);
+        const uint64_t recC = rec_at(s0 + 128 + lane);
+        k4_room(X);
+        const uint32_t tot = ll + ml;
+        const uint32_t inc_tot = wave_scan_incl(tot);
+        const uint32_t inc_ll = wave_scan_incl(ll);
+        const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
+        const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= (int64_t)X.space() - 16);
+        const uint32_t k = (uint32_t)__popcll(fitm);
+        const int kk = k ? (int)k : 1;                 // lanes this batch executes
+        // decode_offset (decoding_context.rs:50-75): fresh offsets (> 3)
+        // are direct; the rare repeat codes walk the batch in order on the
+        // scalar unit, each from the state the fresh offsets before it left.
+        const bool fresh = ofv > 3;
+        const uint64_t val = giant ? OFF_HUGE : (uint64_t)ofv - 3;
+        uint64_t off = val;
+        int derr = 0;
+        uint64_t rm = __ballot(valid && !fresh && lane < kk);
+        uint64_t r0 = rep[0], r1 = rep[1], r2 = rep[2];   // state after lane `prev`
+        int prev = -1;
+        while (rm) {
+          const int ri = __ffsll((long long)rm) - 1;
+          rm &= rm - 1;
+          uint64_t a0, a1, a2;
+          rep_push(val, ri - prev - 1, ri, r0, r1, r2, &a0, &a1, &a2);
+          const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)ofv, ri);
+          const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)ll, ri);
+          uint64_t o = 0;
+          int e = 0;
+          if (oi == 0) {
+            e = ZD_E_NULL_OFFSET;
+          } else {
+            const uint32_t idx = oi - (li != 0 ? 1u : 0u);
+            if (idx == 0) { o = a0; }
+            else if (idx == 1) { o = a1; a1 = a0; a0 = o; }
+            else if (idx == 2) { o = a2; a2 = a1; a1 = a0; a0 = o; }
+            else if (a0 == 0) { e = ZD_E_REF_PANIC; }     // usize underflow of offsets[0] -= 1
+            else { o = a0 - 1; a2 = a1; a1 = a0; a0 = o; }
+          }
+          if (lane == ri) { off = o; derr = e; }
+          r0 = a0; r1 = a1; r2 = a2;
+          prev = ri;
+          if (e) break;                                // the frame stops at this sequence
         }
-        if (lane == ri) { off = o; derr = e; }
-        r0 = a0; r1 = a1; r2 = a2;
-        prev = ri;
-        if (e) break;                                  // the frame stops at this sequence
-      }
-      K4P(1);
-      // checks (decoding_context.rs:86-90, D9)
-      const uint64_t before = (uint64_t)X.pos + opos;
-      const bool dbad = valid && derr != 0;
-      const bool imp = valid && !dbad && ((uint64_t)ll > nl - (lit_cursor + lpos) || lit_cursor + lpos > nl ||
-                                          off > before + ll);
-      const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
-      const uint64_t badm = __ballot(dbad || imp || panic);
-      if (badm) {
-        const int b = __ffsll((long long)badm) - 1;
-        if (b < kk) {
-          const int code = __shfl(dbad ? derr : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
-          err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0 + b, code);
+        K4P(1);
+        // checks (decoding_context.rs:86-90, D9)
+        const uint64_t before = (uint64_t)X.pos + opos;
+        const bool dbad = valid && derr != 0;
+        const bool imp = valid && !dbad && ((uint64_t)lit_cursor + lpos + ll > nl || off > before + ll);
+        const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
+        const uint64_t badm = __ballot(dbad || imp || panic);
+        if (badm) {
+          const int b = __ffsll((long long)badm) - 1;
+          if (b < kk) {
+            const int code = __shfl(dbad ? derr : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
+            err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0 + b, code);
+            break;
+          }
+        }
+        if (k == 0) {                                  // lane 0 alone does not fit the room
+          big = true;
+          bll = (uint32_t)__builtin_amdgcn_readlane((int)ll, 0);
+          bml = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0);
+          boff = readlane_u64(off, 0);
+          rep_push(val, 0 - prev, 1, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
           break;
         }
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
+        const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
+        if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN); break; }
+        // the next batch's literal bytes
+        const u32x4 litB = lit_of(lit_cursor + L);
+        const bool act = (uint32_t)lane < k;
+        __syncthreads();                               // staged literals visible
+        // literals (every lane its own run; from the stage when it holds them)
+        if (act && ll) {
+          l_u8* d = X.at(X.pos + (int32_t)opos);
+          if (!lit_stage || lpos + ll <= 1024) {
+            const l_u8* sp = (const l_u8*)stg + lpos;
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
+          } else {
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
+          }
+        }
+        K4P(2);
+        // matches whose source lies wholly in HBM, flushed two batches ago or
+        // earlier (those stores completed before this batch's waits), copy
+        // at once; the rest in frontier rounds
+        const uint32_t off32 = (uint32_t)(off < 0xFFFFFFFFull ? off : 0xFFFFFFFFull);
+        const int32_t q = X.pos + (int32_t)(opos + ll);
+        const int32_t slo = q - (int32_t)off32;        // act lanes: off <= q (checked above)
+        const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
+        const bool far = act && ml && off32 >= 16 && shi <= (X.hs < fl_safe ? X.hs : fl_safe);
+        if (far) {                                     // ml < off here: no overlap
+          const uint8_t* sp = X.out + slo;
+          const u32x4 v0 = ldg16_nt(sp);
+          const u32x4 v1 = ml > 16 ? ldg16_nt(sp + 16) : v0;
+          l_u8* d = X.at(q);
+          sts_n(d, v0, ml);
+          if (ml > 16) sts_n(d + 16, v1, ml - 16);
+          for (uint32_t x = 32; x < ml; x += 16) sts_n(d + x, ldg16_nt(sp + x), ml - x);
+        }
+        if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
+        uint64_t done = __ballot(!act || ml == 0 || far);
+        __syncthreads();
+        K4P(3);
+        while (done != ~0ull) {
+          const int U = __ffsll((long long)~done) - 1;
+          const int32_t qU = __builtin_amdgcn_readlane(q, U);
+          const bool mine = !((done >> lane) & 1) && (lane == U || shi <= qU);
+          if (mine) {
+            l_u8* d = X.at(q);
+            if (off32 >= 16) {
+              for (uint32_t x = 0; x < ml; x += 16) sts_n(d + x, X.src16(slo + (int32_t)x), ml - x);
+            } else {                             // small period: first 16 bytes bytewise, then 16-byte steps
+              const uint32_t m16 = off32 * ((16 + off32 - 1) / off32);
+              const uint32_t head = ml < 16 ? ml : 16;
+              uint32_t r = 0;
+              for (uint32_t x = 0; x < head; x++) {
+                d[x] = *X.at(slo + (int32_t)r);
+                r = r + 1 == off32 ? 0 : r + 1;
+              }
+              for (uint32_t x = 16; x < ml; x += 16) sts_n(d + x, lds16(d + x - m16), ml - x);
+            }
+          }
+          done |= __ballot(mine);
+          __syncthreads();
+#ifdef ZD_K4_PROF
+          nr++;
+#endif
+        }
+        K4P(4);
+#ifdef ZD_K4_PROF
+        nb++;
+#endif
+        rep_push(val, (int)k - 1 - prev, (int)k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);   // state after lane k - 1
+        lit_cursor += L;
+        X.pos += (int32_t)T;
+        s0 += k;
+        fl_safe = fl_last;
+        fl_last = X.fl;
+        k4_flush(X, false);
+        K4P(5);
+        if (k < 64 || s0 >= n) break;                  // a partial batch: the pipeline restarts at s0
+        recA = recB; winA = winB; recB = recC; litA = litB;
       }
-      if (k == 0) {
+      if (big && err_key == KEY_NONE) {
         // one sequence larger than the window's room: the whole wave copies it
-        const uint32_t ll0 = (uint32_t)__builtin_amdgcn_readlane((int)ll, 0);
-        const uint32_t ml0 = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0);
-        const uint64_t off0 = readlane_u64(off, 0);
-        if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, ll0) || !k4_emit_match(X, (l_u8*)pat, off0, ml0)) {
+        if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, bll) ||
+            !k4_emit_match(X, (l_u8*)pat, (uint32_t)(boff < 0xFFFFFFFFull ? boff : 0xFFFFFFFFull), bml)) {
           err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN);
           break;
         }
-        rep_push(val, 0 - prev, 1, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
-        lit_cursor += ll0;
+        lit_cursor += bll;
         s0 += 1;
-        recA = rec_at(s0 + lane); recB = rec_at(s0 + 64 + lane);
-        winA = win_of(recA, s0 + lane < n);
-        litA = lit_of(lit_cursor);
-        continue;
       }
-      const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
-      const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
-      if (X.pos + (int64_t)T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN); break; }
-      // the next batch's literal bytes
-      const u32x4 litB = lit_of(lit_cursor + L);
-      const bool act = (uint32_t)lane < k;
-      __syncthreads();                                 // staged literals visible
-      // literals (every lane its own run; from the stage when it holds them)
-      if (act && ll) {
-        l_u8* d = X.at(X.pos + opos);
-        if (!lit_stage || lpos + ll <= 1024) {
-          const l_u8* sp = (const l_u8*)stg + lpos;
-          for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
-        } else {
-          for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
-        }
-      }
-      K4P(2);
-      // matches whose source lies wholly in HBM, flushed two batches ago or
-      // earlier (those stores completed before this batch's waits), copy at
-      // once; the rest in frontier rounds
-      const int64_t q = X.pos + opos + ll;
-      const int64_t slo = q - (int64_t)off;
-      const int64_t shi = slo + (int64_t)(off < ml ? off : ml);
-      const bool far = act && ml && off >= 16 && shi <= (X.hs < fl_safe ? X.hs : fl_safe);
-      if (far) {                                       // ml < off here: no overlap
-        const uint8_t* sp = X.out + slo;
-        const u32x4 v0 = ldg16_nt(sp);
-        const u32x4 v1 = ml > 16 ? ldg16_nt(sp + 16) : v0;
-        l_u8* d = X.at(q);
-        sts_n(d, v0, ml);
-        if (ml > 16) sts_n(d + 16, v1, ml - 16);
-        for (uint32_t x = 32; x < ml; x += 16) sts_n(d + x, ldg16_nt(sp + x), ml - x);
-      }
-      if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
-      uint64_t done = __ballot(!act || ml == 0 || far);
-      __syncthreads();
-      K4P(3);
-      while (done != ~0ull) {
-        const int U = __ffsll((long long)~done) - 1;
-        const int64_t qU = readlane_i64(q, U);
-        const bool mine = !((done >> lane) & 1) && (lane == U || shi <= qU);
-        if (mine) {
-          l_u8* d = X.at(q);
-          if (off >= 16) {
-            for (uint32_t x = 0; x < ml; x += 16) sts_n(d + x, X.src16(slo + x), ml - x);
-          } else {                             // small period: first 16 bytes bytewise, then 16-byte steps
-            const uint32_t m16 = (uint32_t)off * ((16 + (uint32_t)off - 1) / (uint32_t)off);
-            const uint32_t head = ml < 16 ? ml : 16;
-            uint32_t r = 0;
-            for (uint32_t x = 0; x < head; x++) {
-              d[x] = *X.at(slo + r);
-              r = r + 1 == off ? 0 : r + 1;
-            }
-            for (uint32_t x = 16; x < ml; x += 16) sts_n(d + x, lds16(d + x - m16), ml - x);
-          }
-        }
-        done |= __ballot(mine);
-        __syncthreads();
-#ifdef ZD_K4_PROF
-        nr++;
-#endif
-      }
-      K4P(4);
-#ifdef ZD_K4_PROF
-      nb++;
-#endif
-      rep_push(val, (int)k - 1 - prev, (int)k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);   // state after lane k - 1
-      lit_cursor += L;
-      X.pos += T;
-      s0 += k;
-      fl_safe = fl_last;
-      fl_last = X.fl;
-      if (k == 64) {
-        recA = recB; winA = winB; recB = recC; litA = litB;
-      } else if (s0 < n) {                             // a partial batch: the pipeline restarts at s0
-        recA = rec_at(s0 + lane); recB = rec_at(s0 + 64 + lane);
-        winA = win_of(recA, s0 + lane < n);
-        litA = lit_of(lit_cursor);
-      }
-      k4_flush(X, false);
-      K4P(5);
     }
     if (err_key != KEY_NONE) break;
     // leftover literals (decoding_context.rs:101-103)
