@@ -1394,6 +1394,21 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           if (e) break;                                // the frame stops at this sequence
         }
         K4P(1);
+        // matches whose source lies wholly in HBM, flushed two batches ago or
+        // earlier (those stores completed before this batch's waits): their
+        // first 32 source bytes are loaded now, to land during the checks
+        // and the literal copies
+        const uint32_t off32 = (uint32_t)(off < 0xFFFFFFFFull ? off : 0xFFFFFFFFull);
+        const int32_t q = X.pos + (int32_t)(opos + ll);
+        const int32_t slo = q - (int32_t)off32;
+        const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
+        const bool far = valid && lane < kk && ml && off32 >= 16 && off32 <= (uint32_t)q &&
+                         shi <= (X.hs < fl_safe ? X.hs : fl_safe);
+        u32x4 fv0, fv1;
+        if (far) {
+          fv0 = ldg16_nt(X.out + slo);
+          if (ml > 16) fv1 = ldg16_nt(X.out + slo + 16);
+        }
         // checks (decoding_context.rs:86-90, D9)
         const uint64_t before = (uint64_t)X.pos + opos;
         const bool dbad = valid && derr != 0;
@@ -1434,22 +1449,13 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           }
         }
         K4P(2);
-        // matches whose source lies wholly in HBM, flushed two batches ago or
-        // earlier (those stores completed before this batch's waits), copy
-        // at once; the rest in frontier rounds
-        const uint32_t off32 = (uint32_t)(off < 0xFFFFFFFFull ? off : 0xFFFFFFFFull);
-        const int32_t q = X.pos + (int32_t)(opos + ll);
-        const int32_t slo = q - (int32_t)off32;        // act lanes: off <= q (checked above)
-        const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
-        const bool far = act && ml && off32 >= 16 && shi <= (X.hs < fl_safe ? X.hs : fl_safe);
-        if (far) {                                     // ml < off here: no overlap
-          const uint8_t* sp = X.out + slo;
-          const u32x4 v0 = ldg16_nt(sp);
-          const u32x4 v1 = ml > 16 ? ldg16_nt(sp + 16) : v0;
+        // far matches from the bytes loaded above (ml < off: no overlap);
+        // the rest in frontier rounds
+        if (far) {
           l_u8* d = X.at(q);
-          sts_n(d, v0, ml);
-          if (ml > 16) sts_n(d + 16, v1, ml - 16);
-          for (uint32_t x = 32; x < ml; x += 16) sts_n(d + x, ldg16_nt(sp + x), ml - x);
+          sts_n(d, fv0, ml);
+          if (ml > 16) sts_n(d + 16, fv1, ml - 16);
+          for (uint32_t x = 32; x < ml; x += 16) sts_n(d + x, ldg16_nt(X.out + slo + x), ml - x);
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
         uint64_t done = __ballot(!act || ml == 0 || far);
