@@ -182,6 +182,16 @@ int zd_plan_results(zd_plan* plan, uint8_t* d_dst, void* stream,
                     int32_t* frame_status, uint64_t* frame_len,
                     uint64_t* total_len, int32_t* first_error_frame);
 
+/* Content checksums, an extra beyond the reference: after zd_plan_results
+ * (same d_dst and stream), XXH64 (seed 0) of every decoded frame's output,
+ * computed on the GPU.  ok[i] = 1 when frame i carries a Content_Checksum and
+ * it equals the digest's low 32 bits, 0 when it differs, -1 when the frame has
+ * none or was not decoded; hash[i] = the digest (0 if not decoded).  The
+ * reference computes the hash but never enforces it (frame.rs:239-255,
+ * SURVEY D5), so a mismatch never changes the decode status.  Host arrays of
+ * plan nframes entries, either may be NULL. */
+int zd_plan_checksums(zd_plan* plan, const uint8_t* d_dst, void* stream, int32_t* ok, uint64_t* hash);
+
 /* Per-kernel time of the last zd_decode_async on the plan, in ms (HIP
  * events recorded between launches when ZD_PROFILE_KERNELS was requested
  * through zd_plan_set_profiling).  names/ms arrays of cap entries. */

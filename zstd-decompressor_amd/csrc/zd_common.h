@@ -168,6 +168,48 @@ ZD_HD inline void rc_compose(const uint32_t a[3], uint32_t b[3]) {
 }
 
 // ---------------------------------------------------------------------------
+// XXH64 (seed 0) pieces, for the content-checksum pass (frame.rs:239-255: the
+// reference computes this hash but never enforces it; verifying it
+// is an extra, reported apart from the decode status).
+// ---------------------------------------------------------------------------
+constexpr uint64_t XP1 = 0x9E3779B185EBCA87ull, XP2 = 0xC2B2AE3D27D4EB4Full, XP3 = 0x165667B19E3779F9ull,
+                   XP4 = 0x85EBCA77C2B2AE63ull, XP5 = 0x27D4EB2F165667C5ull;
+ZD_HD inline uint64_t xx_rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+ZD_HD inline uint64_t xx_round(uint64_t acc, uint64_t in) { return xx_rotl(acc + in * XP2, 31) * XP1; }
+ZD_HD inline uint64_t xx_merge(uint64_t h, uint64_t v) { return (h ^ xx_round(0, v)) * XP1 + XP4; }
+ZD_HD inline uint64_t xx_acc_init(int i) { return i == 0 ? XP1 + XP2 : (i == 1 ? XP2 : (i == 2 ? 0 : 0 - XP1)); }
+// h from the four accumulators (len >= 32) or XP5 (len < 32), then the tail
+// bytes p[0, rem) (rem < 32) and the avalanche
+ZD_HD inline uint64_t xx_finish(uint64_t len, const uint64_t v[4], const uint8_t* p, uint32_t rem) {
+  uint64_t h;
+  if (len >= 32) {
+    h = xx_rotl(v[0], 1) + xx_rotl(v[1], 7) + xx_rotl(v[2], 12) + xx_rotl(v[3], 18);
+    for (int i = 0; i < 4; i++) h = xx_merge(h, v[i]);
+  } else {
+    h = XP5;
+  }
+  h += len;
+  uint32_t i = 0;
+  for (; i + 8 <= rem; i += 8) {
+    uint64_t k = 0;
+    for (int b = 7; b >= 0; b--) k = (k << 8) | p[i + b];
+    h = xx_rotl(h ^ xx_round(0, k), 27) * XP1 + XP4;
+  }
+  if (i + 4 <= rem) {
+    uint64_t k = (uint64_t)p[i] | ((uint64_t)p[i + 1] << 8) | ((uint64_t)p[i + 2] << 16) | ((uint64_t)p[i + 3] << 24);
+    h = xx_rotl(h ^ (k * XP1), 23) * XP2 + XP3;
+    i += 4;
+  }
+  for (; i < rem; i++) h = xx_rotl(h ^ (p[i] * XP5), 11) * XP1;
+  h ^= h >> 33;
+  h *= XP2;
+  h ^= h >> 29;
+  h *= XP3;
+  h ^= h >> 32;
+  return h;
+}
+
+// ---------------------------------------------------------------------------
 // Error keys.  The reference parses every block of a frame (tables included)
 // before decoding any (frame.rs:198-230 then 232-260), and stops at the first
 // error in each phase.  A key orders errors the same way; per frame we keep

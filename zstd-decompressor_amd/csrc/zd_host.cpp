@@ -328,6 +328,8 @@ struct zd_plan {
   bool launched = false;
   // context API hook: comp 0 is a prebuilt "previous block" carrying tables
   bool has_prebuilt = false;
+  // output layout of the last zd_plan_results (frames before the first failure)
+  std::vector<uint64_t> res_off, res_len;
 };
 
 namespace {
@@ -728,9 +730,36 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
     if (tmp) (void)hipFree(tmp);
   }
   if (first < 0 && P->index_status) { first = (int)nf; overall = P->index_status; }
+  P->res_off = to;
+  P->res_len = len;
   if (total_len) *total_len = total;
   if (first_error_frame) *first_error_frame = first;
   return overall;
+}
+
+int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* ok, uint64_t* hash) {
+  if (!P || !P->launched) return ZD_E_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nf = P->fdesc.size(), m = P->res_off.size();   // frames 0..m-1 were decoded
+  std::vector<uint64_t> h(m, 0);
+  if (m) {
+    uint64_t* d = nullptr;
+    HIPCHK(hipMalloc(&d, 3 * m * sizeof(uint64_t)));
+    hipError_t e = hipMemcpy(d, P->res_off.data(), m * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + m, P->res_len.data(), m * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_xxh64(d_dst, d, d + m, (uint32_t)m, d + 2 * m, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), d + 2 * m, m * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return ZD_E_HIP;
+  }
+  for (size_t f = 0; f < nf; f++) {
+    const zd_frame_desc& d = P->frames[f].d;
+    const bool have = f < m && d.kind == ZD_FRAME_ZSTD && d.has_checksum;
+    if (ok) ok[f] = have ? ((uint32_t)h[f] == d.checksum ? 1 : 0) : -1;
+    if (hash) hash[f] = f < m ? h[f] : 0;
+  }
+  return ZD_OK;
 }
 
 int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, uint32_t flags) {

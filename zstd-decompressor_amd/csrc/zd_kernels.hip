@@ -1064,6 +1064,12 @@ __device__ inline int64_t readlane_i64(int64_t x, int l) {
 // Inclusive prefix sum over the 64 lanes (all active) with DPP moves:
 // row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 and 31 across rows.
 
+// per-lane source lane (ds_bpermute)
+__device__ inline uint64_t readlane_any_u64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, l, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), l, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ inline uint64_t readlane_u64(uint64_t x, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
@@ -1981,6 +1987,42 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
     S->rep[1] = L.rep[rb][1];
     S->rep[2] = L.rep[rb][2];
   }
+}
+
+// ---------------------------------------------------------------------------
+// XXH64 of decoded frames (zd_plan_checksums; the reference's frame.rs:
+// 239-255 computes and never enforces it).  Four lanes per frame, one per
+// XXH64 accumulator, 16 frames per wave; lane 0 of a frame folds the four
+// accumulators, hashes the tail and writes the digest.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) const uint64_t g_cu64a1 __attribute__((aligned(1)));
+__global__ __launch_bounds__(64) void zd_k_xxh64(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                 const uint64_t* __restrict__ len, uint32_t n, uint64_t* hash) {
+  const int lane = threadIdx.x, sub = lane & 3;
+  const uint32_t f = blockIdx.x * 16 + (lane >> 2);
+  const bool act = f < n;
+  const uint8_t* p = act ? base + off[f] : base;
+  const uint64_t L = act ? len[f] : 0;
+  const uint64_t nst = L / 32;
+  uint64_t v = xx_acc_init(sub);
+  uint64_t s = 0;
+  for (; s + 4 <= nst; s += 4) {                  // four stripes per trip, loads first
+    const uint64_t w0 = *(g_cu64a1*)(p + 32 * s + 8 * sub), w1 = *(g_cu64a1*)(p + 32 * (s + 1) + 8 * sub);
+    const uint64_t w2 = *(g_cu64a1*)(p + 32 * (s + 2) + 8 * sub), w3 = *(g_cu64a1*)(p + 32 * (s + 3) + 8 * sub);
+    v = xx_round(xx_round(xx_round(xx_round(v, w0), w1), w2), w3);
+  }
+  for (; s < nst; s++) v = xx_round(v, *(g_cu64a1*)(p + 32 * s + 8 * sub));
+  const int l0 = lane & ~3;
+  uint64_t acc[4];
+  for (int i = 0; i < 4; i++) acc[i] = readlane_any_u64(v, l0 + i);
+  if (act && sub == 0) hash[f] = xx_finish(L, acc, p + 32 * nst, (uint32_t)(L - 32 * nst));
+}
+
+hipError_t launch_xxh64(const uint8_t* base, const uint64_t* d_off, const uint64_t* d_len, uint32_t n,
+                        uint64_t* d_hash, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(zd_k_xxh64, dim3((n + 15) / 16), dim3(64), 0, s, base, d_off, d_len, n, d_hash);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -27,6 +27,10 @@ hipError_t launch_pipeline(const LaunchArgs& a);
 hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* d_from,
                           const uint64_t* d_to, const uint64_t* d_len, uint32_t n, hipStream_t s);
 
+// XXH64 of n byte ranges [base + off[i], + len[i]) -> hash[i] (device arrays)
+hipError_t launch_xxh64(const uint8_t* base, const uint64_t* d_off, const uint64_t* d_len, uint32_t n,
+                        uint64_t* d_hash, hipStream_t s);
+
 constexpr int N_KERNELS = 4;
 constexpr uint32_t K4F_CAP = 128u << 10;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];

@@ -57,6 +57,7 @@ SIGNATURES = {
     "zd_decode_async": (C.c_int, [_vp, _vp, _vp, _sz, _vp]),
     "zd_plan_results": (C.c_int, [_vp, _vp, _vp, C.POINTER(C.c_int32), C.POINTER(C.c_uint64),
                                   C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]),
+    "zd_plan_checksums": (C.c_int, [_vp, _vp, _vp, C.POINTER(C.c_int32), C.POINTER(C.c_uint64)]),
     "zd_plan_set_profiling": (C.c_int, [_vp, C.c_int]),
     "zd_plan_kernel_times": (C.c_int, [_vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
     "zd_decompress": (C.c_int, [_vp, _sz, _vp, _sz, _szp, C.c_uint32]),

@@ -90,6 +90,16 @@ class Plan:
             _lib.check(st, "zd_plan_results")
         return st, total.value, list(st_arr)[:nf], list(ln_arr)[:nf], first.value
 
+    def checksums(self, d_dst: int, stream: int = 0):
+        """After results(): (ok per frame: 1 match / 0 mismatch / -1 none, XXH64 digests),
+        computed on the GPU (zd_plan_checksums; an extra, the reference never enforces it)."""
+        nf = self.info.nframes
+        ok = (C.c_int32 * max(nf, 1))()
+        h = (C.c_uint64 * max(nf, 1))()
+        _lib.check(_lib.lib().zd_plan_checksums(self._h, C.c_void_p(d_dst), C.c_void_p(stream), ok, h),
+                   "zd_plan_checksums")
+        return list(ok)[:nf], list(h)[:nf]
+
     def kernel_times(self):
         names = (C.c_char_p * 8)()
         ms = (C.c_float * 8)()
