@@ -1,0 +1,67 @@
+"""Corrupt-input hardening of the C ABI, after the reference's libFuzzer
+target (zstd-decompressor/fuzz/fuzz_targets/fuzz_target_1.rs: iterate the
+frames of arbitrary bytes, decode each, never crash).  Seeded structure-aware
+mutations of valid frames (header fields, block headers, literal/sequence
+section headers, splices, truncations, random tails) go through the GPU path;
+every input must come back with the oracle's status and bytes (or, for inputs
+that decode past their declared size, ZD_E_OUT_OF_DOMAIN), and the process must
+survive all of them."""
+import random
+
+import pytest
+
+from corpus import gen, libzstd
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+OUT_OF_DOMAIN = -91
+
+
+def _seeds():
+    src = gen.text(120_000, seed=5)
+    return [gen.frames(src, 40_000, 1), gen.frames(src, 60_000, 9, checksum=True),
+            gen.frames(gen.xml(50_000, seed=2), 50_000, 19), libzstd.compress(bytes(4000), 3),
+            gen.frames(gen.binary(30_000, seed=3), 30_000, 3)]
+
+
+def _mutate(r: random.Random, seeds):
+    d = bytearray(r.choice(seeds))
+    kind = r.randrange(6)
+    if kind == 0:                       # header region bit flips (frame header, first block header)
+        for _ in range(r.randrange(1, 4)):
+            i = r.randrange(min(len(d), 24))
+            d[i] ^= 1 << r.randrange(8)
+    elif kind == 1:                     # literal / sequence section headers of the first block
+        for _ in range(r.randrange(1, 3)):
+            i = r.randrange(6, min(len(d), 64))
+            d[i] = r.randrange(256)
+    elif kind == 2:                     # random bytes anywhere
+        for _ in range(r.randrange(1, 8)):
+            d[r.randrange(len(d))] = r.randrange(256)
+    elif kind == 3:                     # splice two seeds at random points
+        e = r.choice(seeds)
+        d = d[: r.randrange(len(d))] + e[r.randrange(len(e)):]
+    elif kind == 4:                     # truncation
+        d = d[: r.randrange(len(d))]
+    else:                               # valid magic, random body
+        d = bytearray(b"\x28\xb5\x2f\xfd" + bytes(r.randrange(256) for _ in range(r.randrange(1, 300))))
+    return bytes(d)
+
+
+def test_fuzz_structure_aware():
+    from zstd_decompressor.batch import decompress_status
+    r = random.Random(0xF022)
+    seeds = _seeds()
+    seen = {"ok": 0, "err": 0, "ood": 0}
+    for it in range(600):
+        data = _mutate(r, seeds)
+        p = r.random() < 0.3
+        ost, oout = oracle.decompress_status(data, p)
+        gst, gout = decompress_status(data, p)
+        if gst == OUT_OF_DOMAIN:
+            seen["ood"] += 1
+            continue
+        assert gst == ost, f"#{it}: oracle {ost}, gpu {gst}"
+        assert gout == oout, f"#{it}: output differs"
+        seen["ok" if ost == 0 else "err"] += 1
+    assert seen["ood"] <= 30, seen

@@ -431,12 +431,18 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
   if (C.lit_type == LIT_COMPRESSED && C.host_stage > PS_HUF_DESC) {
     int p = 0;
     const int st = k1_huffman_lane(blk + C.lit_data, src, src + src_size, L, luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
-    if (st) {
-      const uint32_t ph = (st == ZD_E_OUT_OF_DOMAIN) ? PH_LIMIT : PH_PARSE;
-      key_min(fstate, C.frame, make_key(ph, C.block_in_frame, PS_HUF_DESC, 0, st));
+    if (st == ZD_E_OUT_OF_DOMAIN) {
+      // the tree parsed (the reference's Block::parse goes on to the
+      // sequences section) but no GPU LUT holds it: out of domain where the
+      // reference would decode these literals, after every parse error of
+      // the frame and every decode error of the blocks before
+      key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
+    } else if (st) {
+      key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_HUF_DESC, 0, st));
       return;                                     // Block::parse stops at the literals section
+    } else {
+      cstate[ci].huf_bits = (uint8_t)p;
     }
-    cstate[ci].huf_bits = (uint8_t)p;
   }
   if (C.nseq > 0 && C.host_stage > PS_SEQ_TABLES) {
     uint8_t al[3] = {0, 0, 0};
@@ -662,7 +668,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     }
     const bool fits = total <= R + 16;          // the block's literal slot (host: R + 16 bytes)
     if (!rfc && !err && !fits)
-      key_min(fstate, C.frame, make_key(PH_LIMIT, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
+      key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
     redo[b] = !rfc && !err && fits;
     cstate[ci].lit_count = total;
     if (err || (!rfc && !fits)) cstate[ci].stop = 1;
