@@ -328,6 +328,9 @@ struct zd_plan {
   bool launched = false;
   // context API hook: comp 0 is a prebuilt "previous block" carrying tables
   bool has_prebuilt = false;
+  // second stream for K2 beside K3 (created on first launch)
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   // output layout of the last zd_plan_results (frames before the first failure)
   std::vector<uint64_t> res_off, res_len;
 };
@@ -626,6 +629,9 @@ void zd_plan_destroy(zd_plan* P) {
   if (P->d_ws) (void)hipFree(P->d_ws);
   if (P->d_staging) (void)hipFree(P->d_staging);
   if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
+  if (P->fork) (void)hipEventDestroy(P->fork);
+  if (P->join) (void)hipEventDestroy(P->join);
+  if (P->aux) (void)hipStreamDestroy(P->aux);
   delete P;
 }
 
@@ -675,6 +681,15 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
+  // K2 beside K3 on a second stream measured slower on C4 (61.4 vs 57.9 ms:
+  // K3 is LDS-bound and K2 takes its CUs), so it is opt-in (ZD_FORK=1)
+  static const bool fork = getenv("ZD_FORK") && atoi(getenv("ZD_FORK")) == 1;
+  if (!P->aux && fork) {
+    HIPCHK(hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&P->fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&P->join, hipEventDisableTiming));
+  }
+  a.aux = P->aux; a.fork = P->fork; a.join = P->join;
   if (const char* g = getenv("ZD_K4_GRID")) a.k4_grid = (uint32_t)strtoul(g, nullptr, 0);
   HIPCHK(launch_pipeline(a));
   P->launched = true;

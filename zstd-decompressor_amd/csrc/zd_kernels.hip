@@ -2064,14 +2064,26 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_tables, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
                        a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
+  // K2 and K3 are independent once K1 is done: K2 runs on the aux stream
+  // beside K3 (not when timing kernels one by one)
+  const bool fork = a.aux && !a.events && a.n_huf && a.n_seq && (a.kmask & 6) == 6;
+  hipStream_t s2 = fork ? a.aux : s;
+  if (fork) {
+    if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
+  }
   if (a.n_huf && (a.kmask & 2))
-    hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s, a.src, comp,
+    hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s2, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
+  if (fork)
+    if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   if (a.n_seq && (a.kmask & 4))
     hipLaunchKernelGGL(zd_k_sequences, dim3((a.n_seq + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses,
                        seqs);
+  if (fork)
+    if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   if (a.n_frames > a.n_k4f && (a.kmask & 8))     // frames on the streaming K4 (the rest exit at once)
     hipLaunchKernelGGL(zd_k_execute, dim3(a.k4_grid && a.k4_grid < a.n_frames ? a.k4_grid : a.n_frames), dim3(64), 0,

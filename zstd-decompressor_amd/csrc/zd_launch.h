@@ -16,6 +16,8 @@ struct LaunchArgs {
   uint32_t n_tables, n_huf, n_seq, n_frames, n_k4f;
   hipStream_t stream;
   hipEvent_t* events;      // optional: 5 events recorded around the 4 kernels
+  hipStream_t aux = nullptr;   // optional second stream: K2 beside K3
+  hipEvent_t fork = nullptr, join = nullptr;
   uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
   uint32_t k4_grid = 0;    // cap on K4 workgroups (persistent over frames); 0 = one per frame
 };
