@@ -1094,6 +1094,15 @@ __device__ inline void rep_push(uint64_t val, int cnt, int end, uint64_t r0, uin
 
 // Frame positions are 32-bit: frames with sequences stay below MAX_FRAME_OUT
 // (2^27) and the planner caps every frame the streaming K4 runs below 2^31.
+// K4's workgroup is one wave: LDS operations of a wave execute in order, so
+// ordering between its own LDS writes and reads needs no lgkmcnt drain or
+// s_barrier, only that the compiler keeps program order.
+__device__ inline void k4_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct K4 {
   l_u8* buf;
   uint8_t* out;            // frame output (frame position 0)
@@ -1144,7 +1153,7 @@ __device__ void k4_room(K4& X) {
     if (x < n) *(l_u32x4a1*)(X.buf + x) = v;
     __builtin_amdgcn_wave_barrier();
   }
-  __syncthreads();
+  k4_sync();
   X.hs = nh;
 }
 
@@ -1160,7 +1169,7 @@ __device__ bool k4_emit_lits(K4& X, const uint8_t* s, uint32_t fill, uint32_t n)
       const u32x4 v = s ? ldg16(s + x) : f4;
       sts_n(X.at(X.pos + x), v, (uint32_t)(chunk - x));
     }
-    __syncthreads();
+    k4_sync();
     X.pos += chunk;
     if (s) s += chunk;
     n -= (uint32_t)chunk;
@@ -1181,7 +1190,7 @@ __device__ bool k4_emit_match(K4& X, l_u8* pat, uint32_t off, uint32_t n) {
   const bool need_hbm = !small && q - (int32_t)off < X.hs;
   if (small) {                                 // q - off >= hs here: the period is in the window
     if (X.lane < 48) pat[X.lane] = *X.at(q - (int32_t)off + (int32_t)((uint32_t)X.lane % off));
-    __syncthreads();
+    k4_sync();
   }
   if (__ballot(need_hbm)) wait_vm();
   while (j0 < n) {
@@ -1203,7 +1212,7 @@ __device__ bool k4_emit_match(K4& X, l_u8* pat, uint32_t off, uint32_t n) {
         }
       }
     }
-    __syncthreads();
+    k4_sync();
     X.pos += chunk;
     j0 += (uint32_t)chunk;
     k4_flush(X, false);
@@ -1260,7 +1269,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     // existing output's tail comes back from HBM)
     X.hs = X.alignd(X.pos > K4_W ? X.pos - K4_W : 0);
     for (int32_t p = (X.hs > 0 ? X.hs : 0) + lane; p < X.pos; p += 64) *X.at(p) = X.out[p];
-    __syncthreads();
+    k4_sync();
   }
   uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
   uint64_t err_key = KEY_NONE;
@@ -1309,7 +1318,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const int cnt = 1 << cstate[s].al[k];
         for (int e = lane; e < cnt; e += 64) stab[k][e] = (uint8_t)(g[e] & 63);
       }
-      __syncthreads();
+      k4_sync();
     }
     // Software pipeline over batches of 64 sequences: the records two
     // batches ahead, the bitstream windows of the next batch and its literal
@@ -1449,7 +1458,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         // the next batch's literal bytes
         const u32x4 litB = lit_of(lit_cursor + L);
         const bool act = (uint32_t)lane < k;
-        __syncthreads();                               // staged literals visible
+        k4_sync();                               // staged literals visible
         // literals (every lane its own run; from the stage when it holds them)
         if (act && ll) {
           l_u8* d = X.at(X.pos + (int32_t)opos);
@@ -1471,7 +1480,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
         uint64_t done = __ballot(!act || ml == 0 || far);
-        __syncthreads();
+        k4_sync();
         K4P(3);
         while (done != ~0ull) {
           const int U = __ffsll((long long)~done) - 1;
@@ -1493,7 +1502,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
             }
           }
           done |= __ballot(mine);
-          __syncthreads();
+          k4_sync();
 #ifdef ZD_K4_PROF
           nr++;
 #endif
@@ -1547,7 +1556,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     S->rep[1] = rep[1];
     S->rep[2] = rep[2];
   }
-  __syncthreads();                               // the window is reused by the next frame
+  k4_sync();                               // the window is reused by the next frame
   }
 }
 
