@@ -1031,12 +1031,12 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
 #define ZD_K4_W 2048
 #endif
 #ifndef ZD_K4_B
-#define ZD_K4_B 2048
+#define ZD_K4_B 1792
 #endif
 constexpr int K4_W = ZD_K4_W;                 // history kept after a slide
 constexpr int K4_B = ZD_K4_B;                 // room kept for a batch (a slide when less is left)
 #ifndef ZD_K4_C
-#define ZD_K4_C (8192 + 32)
+#define ZD_K4_C 7200
 #endif
 constexpr int K4_C = ZD_K4_C;                 // window bytes
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1244,7 +1244,7 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 }
 
 #ifndef ZD_K4_MINW
-#define ZD_K4_MINW 1
+#define ZD_K4_MINW 4
 #endif
 __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __restrict__ src, uint8_t* outbase,
                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
