@@ -712,6 +712,8 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
 constexpr int K3_LANES = ZD_K3_LANES;
 #ifdef ZD_K3_W1
 #define K3_CHAIN seq_chain       // window one step ahead (reference variant for experiments)
+#elif defined(ZD_K3_W3)
+#define K3_CHAIN seq_chain3      // window three steps ahead
 #else
 #define K3_CHAIN seq_chain2      // window two steps ahead (default: 23.8 -> 18.3 ms on C4)
 #endif
@@ -931,6 +933,105 @@ __device__ int seq_chain2(const uint8_t* bs, uint32_t bs_size, uintptr_t base, T
     const bool d1 = step(wa, true);
     const bool d2 = step(wb, !d1);
     if (d2) break;
+  }
+  return st;
+}
+
+// The chain with the window loaded three steps ahead: a 40-byte window
+// ending at the byte of pos_{i+1} covers every bit steps i+1..i+3 read
+// (3 x 90 bits + 7), at the price of a 10-way dword select per step.
+struct Win10 {
+  uint32_t w[10];
+  int32_t wb;
+};
+__device__ inline Win10 win10_load(const uint8_t* s, int32_t m, int32_t pos) {
+  const int32_t tb = (pos + 7) >> 3;
+  const int32_t o = max(tb - 40, m);
+  const u32x4ua v0 = *(g_u32x4ua*)(s + o);
+  const u32x4ua v1 = *(g_u32x4ua*)(s + o + 16);
+  const u32x2ua v2 = *(g_u32x2ua*)(s + o + 32);
+  Win10 w;
+  w.w[0] = v0.x; w.w[1] = v0.y; w.w[2] = v0.z; w.w[3] = v0.w;
+  w.w[4] = v1.x; w.w[5] = v1.y; w.w[6] = v1.z; w.w[7] = v1.w;
+  w.w[8] = v2.x; w.w[9] = v2.y;
+  w.wb = o * 8;
+  return w;
+}
+__device__ inline uint32_t win10_bits(const Win10& w, int32_t p, uint32_t S) {
+  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
+  const uint32_t k = y >> 5;
+  uint32_t lo = w.w[0], hi = w.w[1];
+#pragma unroll
+  for (int i = 1; i < 10; i++) {
+    lo = k >= (uint32_t)i ? w.w[i] : lo;
+    hi = k >= (uint32_t)i ? (i + 1 < 10 ? w.w[i + 1] : 0u) : hi;
+  }
+  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
+}
+
+template <typename TP, bool K3_SYM>
+__device__ int seq_chain3(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
+                          int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
+  if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return ZD_E_NULL_BYTE;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
+  const int32_t A = all + alo + alm;
+  if (A > pos) return ZD_E_NOT_ENOUGH_BITS;
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-40);
+  const int32_t pos0 = pos;
+  const Win10 wi = win10_load(bs, m, pos);
+  const uint32_t v0 = win10_bits(wi, pos, (uint32_t)A);
+  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
+  pos -= A;
+  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
+  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
+  // loop entry mirrors the loop's memory-op order (window, store) x 3
+  Win10 wa = win10_load(bs, m, pos0);            // step 0
+  asm volatile("" ::: "memory");
+  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+  Win10 wb = win10_load(bs, m, pos);             // step 1
+  asm volatile("" ::: "memory");
+  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+  Win10 wc = win10_load(bs, m, pos);             // step 2 (pos_2 >= pos_0 - 180)
+  asm volatile("" ::: "memory");
+  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+  int st = 0;
+  uint32_t i = 0;
+  auto step = [&](Win10& use, bool live) -> bool {
+    uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
+    if (K3_SYM) {
+      eLL = k3_entry(eLL, 0);
+      eOF = k3_entry(eOF, 1);
+      eML = k3_entry(eML, 2);
+    }
+    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
+    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
+    const uint32_t E = ((eLL >> 10) & 31) + ((eML >> 10) & 31) + ((eOF >> 10) & 31);
+    const bool codemax = ((eLL | eML | eOF) & K3_BAD) != 0;
+    const bool last = i + 1 >= n;
+    const uint32_t S = last ? 0 : nbL + nbM + nbO;
+    const int sst = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : ((int32_t)(E + S) > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
+    st = live ? sst : st;
+    const int32_t p2 = pos - (int32_t)E;
+    const uint32_t v = win10_bits(use, p2, S);
+    pos = p2 - (int32_t)S;
+    use = win10_load(bs, m, pos);                  // for step i + 3
+    const uint32_t vO = __builtin_amdgcn_ubfe(v, 0, nbO), vM = __builtin_amdgcn_ubfe(v, nbO, nbM);
+    const uint32_t vL = v >> (nbO + nbM);
+    sLL = (nsL << nbL) + vL - TL;
+    sML = (nsM << nbM) + vM - TM;
+    sOF = (nsO << nbO) + vO - TO;
+    asm volatile("" ::: "memory");
+    k3_store(out + (live ? i + 1 : n), (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+    i++;
+    return !live || sst != 0 || last;
+  };
+  for (;;) {
+    const bool d1 = step(wa, true);
+    const bool d2 = step(wb, !d1);
+    const bool d3 = step(wc, !d2);
+    if (d3) break;
   }
   return st;
 }
