@@ -39,9 +39,8 @@ def make_corpus(workload: str, unique_bytes: int, seed: int):
     from corpus import gen
     t0 = time.time()
     if workload == "c2":
-        src = None
-        data = gen.c2_raw_rle(64 << 20)
-        return data, None, 1, {"frames": 1, "frame_bytes": 64 << 20}, time.time() - t0
+        data, src = gen.c2_raw_rle(64 << 20, with_content=True)
+        return data, src, 1, {"frames": 1, "frame_bytes": 64 << 20}, time.time() - t0
     if workload == "c5":
         src = gen.text(unique_bytes, seed=seed)
         data = gen.frames(src, 1 << 20, 9)

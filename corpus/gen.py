@@ -133,21 +133,28 @@ def binary(nbytes: int, seed: int = SEED + 2) -> bytes:
     return b"".join(out)[:nbytes]
 
 
-def c2_raw_rle(total: int = 64 << 20, block: int = 128 << 10, seed: int = SEED + 3) -> bytes:
+def c2_raw_rle(total: int = 64 << 20, block: int = 128 << 10, seed: int = SEED + 3,
+               with_content: bool = False):
     """C2: one frame, not single-segment (window descriptor 0x68 = 8 MiB),
     4-byte FCS, alternating Raw (random bytes) / RLE (byte = index & 0xFF)
-    blocks, no checksum."""
+    blocks, no checksum.  with_content: (frame bytes, the content they carry)."""
     rng = np.random.default_rng(seed)
     nb = total // block
     out = [struct.pack("<I", 0xFD2FB528), bytes([0x80, 0x68]), struct.pack("<I", total)]
+    content = []
     for i in range(nb):
         last = 1 if i == nb - 1 else 0
         if i % 2 == 0:
             out.append(struct.pack("<I", last | (0 << 1) | (block << 3))[:3])
-            out.append(rng.integers(0, 256, size=block, dtype=np.uint8).tobytes())
+            raw = rng.integers(0, 256, size=block, dtype=np.uint8).tobytes()
+            out.append(raw)
+            content.append(raw)
         else:
             out.append(struct.pack("<I", last | (1 << 1) | (block << 3))[:3])
             out.append(bytes([i & 0xFF]))
+            content.append(bytes([i & 0xFF]) * block)
+    if with_content:
+        return b"".join(out), b"".join(content)
     return b"".join(out)
 
 

@@ -292,7 +292,18 @@ struct FrameDesc {
   uint32_t first_block;    // into BlockRec[]
   uint32_t nblocks;        // blocks to execute (0 for frames skipped by parse errors)
   uint32_t lds;            // 1: executed by K4F (whole frame in LDS), 0: by the streaming K4
-  uint32_t _pad;
+  uint32_t skip;           // leading raw/RLE blocks copied by K0 (the streaming K4 starts after them)
+  uint64_t skip_bytes;     // their output bytes
+};
+
+// K0: one piece (<= COPY_PIECE bytes) of a raw / RLE block whose output offset
+// is known at plan time (every block before it in the frame is raw or RLE).
+constexpr uint32_t COPY_PIECE = 32u << 10;
+struct CopyDesc {
+  uint64_t src;            // absolute offset of the bytes in d_src (raw)
+  uint64_t dst;            // absolute offset in the output base
+  uint32_t size;
+  uint32_t fill;           // 0x100 | byte for RLE, 0 for raw
 };
 
 struct FrameState {
@@ -305,6 +316,7 @@ struct FrameState {
 struct Workspace {
   uint64_t comp, comp_state, blocks, frames, frame_state;
   uint64_t list_tables, list_huf, list_seq, list_k4f;   // u32 work lists
+  uint64_t copies;                                      // CopyDesc[] for K0
   uint64_t lits, seqs, luts, fses;
   uint64_t total;
 };

@@ -314,6 +314,7 @@ struct zd_plan {
   std::vector<FrameDesc> fdesc;
   std::vector<FrameState> fstate0;
   std::vector<uint32_t> list_tables, list_huf, list_seq, list_k4f;
+  std::vector<CopyDesc> copies;         // K0 pieces
   std::vector<uint64_t> frame_cap_off;   // output offset per frame (capacity layout)
   zd_plan_info info{};
   Workspace W{};
@@ -346,7 +347,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   uint64_t lits = 0, nseq_total = 0, nrec = 0, out_off = 0;
   uint32_t lut_slots = 0, fse_slots = 0;
   bool exact = true;
-  P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear();
+  P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
   P->frame_cap_off.clear();
   for (size_t fi = 0; fi < P->frames.size(); fi++) {
     HostFrame& hf = P->frames[fi];
@@ -457,6 +458,29 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     static const bool k4f_on = getenv("ZD_K4F") && atoi(getenv("ZD_K4F")) == 1;
     fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
     if (fd.lds) P->list_k4f.push_back((uint32_t)fi);
+    // Leading raw / RLE blocks (skippable payloads too) have output offsets
+    // known here: K0 copies them in parallel pieces, the streaming K4 starts
+    // after them (a frame of raw/RLE blocks only never reaches K4's loop).
+    if (!fd.lds && fd.nblocks && cap < 0x7FF00000ull) {
+      uint64_t pre = 0;
+      uint32_t k = 0;
+      for (; k < fd.nblocks; k++) {
+        const BlockRec& br = P->blocks[fd.first_block + k];
+        if (br.type != 0 && br.type != 1 && br.type != 4) break;
+        if (out_len0 + pre + br.size > cap) break;
+        for (uint64_t x = 0; x < br.size; x += COPY_PIECE) {
+          CopyDesc c{};
+          c.src = br.src + (br.type == 1 ? 0 : x);
+          c.dst = out_off + out_len0 + pre + x;
+          c.size = (uint32_t)std::min<uint64_t>(COPY_PIECE, br.size - x);
+          c.fill = br.type == 1 ? (0x100u | br.rle) : 0u;
+          P->copies.push_back(c);
+        }
+        pre += br.size;
+      }
+      fd.skip = k;
+      fd.skip_bytes = pre;
+    }
     P->frame_cap_off.push_back(out_off);
     out_off += cap;
     P->fdesc.push_back(fd);
@@ -475,6 +499,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
   W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
   W.list_k4f = carve(4 * std::max<size_t>(P->list_k4f.size(), 1));
+  W.copies = carve(sizeof(CopyDesc) * std::max<size_t>(P->copies.size(), 1));
   W.lits = carve(lits + 64);
   W.seqs = carve(8 * nrec + 64);
   W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
@@ -507,6 +532,7 @@ int upload_plan(zd_plan* P) {
   if (int r = up(P->W.list_huf, P->list_huf.data(), P->list_huf.size() * 4)) return r;
   if (int r = up(P->W.list_seq, P->list_seq.data(), P->list_seq.size() * 4)) return r;
   if (int r = up(P->W.list_k4f, P->list_k4f.data(), P->list_k4f.size() * 4)) return r;
+  if (int r = up(P->W.copies, P->copies.data(), P->copies.size() * sizeof(CopyDesc))) return r;
   if (!P->info.out_exact) {
     P->staging_bytes = P->info.out_bytes;
     HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
@@ -678,6 +704,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_seq = (uint32_t)P->list_seq.size();
   a.n_frames = (uint32_t)P->fdesc.size();
   a.n_k4f = (uint32_t)P->list_k4f.size();
+  a.n_copies = (uint32_t)P->copies.size();
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
@@ -908,6 +935,7 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   a.n_seq = (uint32_t)P->list_seq.size();
   a.n_frames = 1;
   a.n_k4f = (uint32_t)P->list_k4f.size();
+  a.n_copies = (uint32_t)P->copies.size();
   a.stream = nullptr;
   if (launch_pipeline(a) != hipSuccess) return fin(ZD_E_HIP);
   if (hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
@@ -1114,6 +1142,7 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   a.src = d_src; a.src_size = nlits; a.out = c->d_out; a.ws = P.d_ws; a.W = P.W;
   a.n_frames = 1;
   a.n_k4f = (uint32_t)P.list_k4f.size();
+  a.n_copies = (uint32_t)P.copies.size();
   if (launch_pipeline(a) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
   FrameState st{};
   if (hipMemcpy(&st, P.d_ws + P.W.frame_state, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return fin(ZD_E_HIP);

@@ -21,7 +21,8 @@
 
 namespace zd {
 
-const char* const kKernelNames[N_KERNELS] = {"zd_k_tables", "zd_k_huffman", "zd_k_sequences", "zd_k_execute"};
+const char* const kKernelNames[N_KERNELS] = {"zd_k_rawcopy", "zd_k_tables", "zd_k_huffman", "zd_k_sequences",
+                                             "zd_k_execute"};
 
 // ---------------------------------------------------------------------------
 // constants (decoders/sequence.rs:95-191, sequences.rs:29-39)
@@ -1373,7 +1374,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   X.out = outbase + F.out;
   X.a0 = (int32_t)((16 - ((uintptr_t)X.out & 15)) & 15);
   X.lane = lane;
-  X.pos = (int32_t)F.out_len0;
+  X.pos = (int32_t)(F.out_len0 + F.skip_bytes);    // K0 wrote the leading raw/RLE blocks
   X.fl = X.pos;
   X.cap = (int32_t)(F.out_cap < 0x7FFFFFF0ull ? F.out_cap : 0x7FFFFFF0ull);
   {
@@ -1395,7 +1396,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
 #define K4P(i) do { } while (0)
 #endif
 
-  for (uint32_t j = 0; j < F.nblocks && err_key == KEY_NONE; j++) {
+  for (uint32_t j = F.skip; j < F.nblocks && err_key == KEY_NONE; j++) {
     const BlockRec B = blocks[F.first_block + j];
     if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
     if (B.type == 5) continue;
@@ -2121,6 +2122,30 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 }
 
 // ---------------------------------------------------------------------------
+// K0: raw / RLE blocks at the head of a frame (block.rs:78-79: Raw appends
+// the bytes, RLE the byte `size` times), whose output offsets the planner
+// knows.  One 256-thread workgroup per piece of <= 32 KiB: 16-byte loads,
+// 16-byte aligned stores, head and tail bytewise.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void zd_k_rawcopy(const uint8_t* __restrict__ src, uint8_t* outbase,
+                                                    const CopyDesc* __restrict__ copies) {
+  const CopyDesc c = copies[blockIdx.x];
+  const uint8_t* s = src + c.src;
+  uint8_t* d = outbase + c.dst;
+  const bool rle = c.fill != 0;
+  const uint8_t b = (uint8_t)c.fill;
+  const uint32_t f = b * 0x01010101u;
+  const u32x4 f4 = (u32x4){f, f, f, f};
+  const uint32_t head = min(c.size, (uint32_t)((16 - ((uintptr_t)d & 15)) & 15));
+  const int t = threadIdx.x;
+  if ((uint32_t)t < head) d[t] = rle ? b : s[t];
+  uint32_t x = head + 16 * t;
+  for (; x + 16 <= c.size; x += 16 * 256) *(g_u32x4*)(d + x) = rle ? f4 : ldg16(s + x);
+  const uint32_t tail0 = head + ((c.size - head) & ~15u);
+  if (tail0 + t < c.size) d[tail0 + t] = rle ? b : s[tail0 + t];
+}
+
+// ---------------------------------------------------------------------------
 // XXH64 of decoded frames (zd_plan_checksums; the reference's frame.rs:
 // 239-255 computes and never enforces it).  Four lanes per frame, one per
 // XXH64 accumulator, 16 frames per wave; lane 0 of a frame folds the four
@@ -2185,10 +2210,14 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   hipStream_t s = a.stream;
   hipError_t e;
   if (a.events) if ((e = hipEventRecord(a.events[0], s)) != hipSuccess) return e;
+  if (a.n_copies && (a.kmask & 8))
+    hipLaunchKernelGGL(zd_k_rawcopy, dim3(a.n_copies), dim3(256), 0, s, a.src, a.out,
+                       (const CopyDesc*)(ws + W.copies));
+  if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
   if (a.n_tables && (a.kmask & 1))
     hipLaunchKernelGGL(zd_k_tables, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
                        a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
-  if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
+  if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   // K2 and K3 are independent once K1 is done: K2 runs on the aux stream
   // beside K3 (not when timing kernels one by one)
   const bool fork = a.aux && !a.events && a.n_huf && a.n_seq && (a.kmask & 6) == 6;
@@ -2202,14 +2231,14 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
   if (fork)
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
-  if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
+  if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   if (a.n_seq && (a.kmask & 4))
     hipLaunchKernelGGL(zd_k_sequences, dim3((a.n_seq + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses,
                        seqs);
   if (fork)
     if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-  if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
+  if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
   if (a.n_frames > a.n_k4f && (a.kmask & 8))     // frames on the streaming K4 (the rest exit at once)
     hipLaunchKernelGGL(zd_k_execute, dim3(a.k4_grid && a.k4_grid < a.n_frames ? a.k4_grid : a.n_frames), dim3(64), 0,
                        s, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
@@ -2218,7 +2247,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_execute_lds, dim3(a.n_k4f), dim3(K4F_T), 0, s, a.src, a.out, frames, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses, (const uint32_t*)(ws + W.list_k4f));
-  if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
+  if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;
   return hipGetLastError();
 }
 

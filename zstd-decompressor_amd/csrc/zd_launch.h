@@ -13,9 +13,9 @@ struct LaunchArgs {
   uint8_t* out;            // output base (d_dst or the plan's staging buffer)
   uint8_t* ws;             // workspace base
   Workspace W;
-  uint32_t n_tables, n_huf, n_seq, n_frames, n_k4f;
+  uint32_t n_tables, n_huf, n_seq, n_frames, n_k4f, n_copies;
   hipStream_t stream;
-  hipEvent_t* events;      // optional: 5 events recorded around the 4 kernels
+  hipEvent_t* events;      // optional: N_KERNELS + 1 events recorded around the kernels
   hipStream_t aux = nullptr;   // optional second stream: K2 beside K3
   hipEvent_t fork = nullptr, join = nullptr;
   uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
@@ -33,7 +33,7 @@ hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* 
 hipError_t launch_xxh64(const uint8_t* base, const uint64_t* d_off, const uint64_t* d_len, uint32_t n,
                         uint64_t* d_hash, hipStream_t s);
 
-constexpr int N_KERNELS = 4;
+constexpr int N_KERNELS = 5;
 constexpr uint32_t K4F_CAP = 128u << 10;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];
 
