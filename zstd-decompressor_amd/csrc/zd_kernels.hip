@@ -14,6 +14,7 @@
 //                      HBM (replaces decoding_context.rs:50-106 + block.rs:74-99)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "../../include/zd.h"
 #include "zd_common.h"
@@ -503,6 +504,96 @@ __device__ inline uint64_t winu_top(const WinU& w, uint32_t d) {
   return k < 64 ? f : (w.w0 << (k & 63));
 }
 
+// 128-bit window of a backward bitstream: bits [wb, wb + 128) of the stream
+// (bit 0 = LSB of byte 0), loaded unaligned as the 16 bytes ending at the
+// byte that holds bit pos - 1, clamped at the input base.
+typedef uint32_t u32x4ua __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4ua g_u32x4ua;
+struct Win4 {
+  uint32_t w0, w1, w2, w3;
+  int32_t wb;
+};
+// m = base - s (<= 0): the lowest byte offset the window may start at.
+__device__ inline Win4 win4_load(const uint8_t* s, int32_t m, int32_t pos) {
+  const int32_t tb = (pos + 7) >> 3;
+  const int32_t o = max(tb - 16, m);
+  const u32x4ua v = *(g_u32x4ua*)(s + o);
+  Win4 w;
+  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w;
+  w.wb = o * 8;
+  return w;
+}
+// The S bits [p - S, p) of the stream, S <= 32, MSB-first value; requires
+// wb <= p - S and p <= wb + 128 (else garbage, never a memory access).
+__device__ inline uint32_t win4_bits(const Win4& w, int32_t p, uint32_t S) {
+  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
+  const uint32_t k = y >> 5;
+  uint32_t lo = k == 0 ? w.w0 : w.w1;
+  uint32_t hi = k == 0 ? w.w1 : w.w2;
+  lo = k >= 2 ? w.w2 : lo;
+  hi = k >= 2 ? w.w3 : hi;
+  lo = k >= 3 ? w.w3 : lo;
+  hi = k >= 3 ? 0u : hi;
+  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
+}
+
+// The same chain with the bitstream window loaded two steps ahead: a
+// 24-byte window ending at the byte of pos_{i+1} covers every bit steps
+// i+1 and i+2 read (each step reads at most 63 extra + 27 state bits), so a
+// window load has a whole step more to land.
+struct Win6 {
+  uint32_t w0, w1, w2, w3, w4, w5;
+  int32_t wb;
+};
+typedef uint32_t u32x2ua __attribute__((ext_vector_type(2), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x2ua g_u32x2ua;
+__device__ inline Win6 win6_load(const uint8_t* s, int32_t m, int32_t pos) {
+  const int32_t tb = (pos + 7) >> 3;
+  const int32_t o = max(tb - 24, m);
+  const u32x4ua v = *(g_u32x4ua*)(s + o);
+  const u32x2ua u = *(g_u32x2ua*)(s + o + 16);
+  Win6 w;
+  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w; w.w4 = u.x; w.w5 = u.y;
+  w.wb = o * 8;
+  return w;
+}
+__device__ inline uint32_t win6_bits(const Win6& w, int32_t p, uint32_t S) {
+  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
+  const uint32_t k = y >> 5;
+  uint32_t lo = k == 0 ? w.w0 : w.w1;
+  uint32_t hi = k == 0 ? w.w1 : w.w2;
+  lo = k >= 2 ? w.w2 : lo;
+  hi = k >= 2 ? w.w3 : hi;
+  lo = k >= 3 ? w.w3 : lo;
+  hi = k >= 3 ? w.w4 : hi;
+  lo = k >= 4 ? w.w4 : lo;
+  hi = k >= 4 ? w.w5 : hi;
+  lo = k >= 5 ? w.w5 : lo;
+  hi = k >= 5 ? 0u : hi;
+  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
+}
+
+#ifdef ZD_K2_W1
+constexpr bool K2_WIN2 = false;   // experiment: K2 windows one group ahead only
+#else
+constexpr bool K2_WIN2 = true;
+#endif
+
+// The 64 bits below q of a 24-byte window, MSB-first (q - 32 >= wb, q <= wb + 192;
+// bits below the window read as zero: K2 looks at the top 44 only).
+__device__ inline uint64_t win6_top64(const Win6& w, int32_t q) {
+  const uint32_t y = (uint32_t)(q - 32 - w.wb);          // bit offset of the top dword's low end
+  const uint32_t k = y >> 5, sh = y & 31;                // k in [0, 5]
+  uint32_t a = 0u, b = w.w0, c = w.w1;                   // w[k-1], w[k], w[k+1]
+  a = k >= 1 ? w.w0 : a; b = k >= 1 ? w.w1 : b; c = k >= 1 ? w.w2 : c;
+  a = k >= 2 ? w.w1 : a; b = k >= 2 ? w.w2 : b; c = k >= 2 ? w.w3 : c;
+  a = k >= 3 ? w.w2 : a; b = k >= 3 ? w.w3 : b; c = k >= 3 ? w.w4 : c;
+  a = k >= 4 ? w.w3 : a; b = k >= 4 ? w.w4 : b; c = k >= 4 ? w.w5 : c;
+  a = k >= 5 ? w.w4 : a; b = k >= 5 ? w.w5 : b; c = k >= 5 ? 0u : c;
+  const uint32_t hi = __builtin_amdgcn_alignbit(c, b, sh), lo = __builtin_amdgcn_alignbit(b, a, sh);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // ---------------------------------------------------------------------------
 // K2: Huffman literals (literals.rs:49-86 + huffman.rs:205-218), one STREAM
 // per lane: a workgroup (one wave) takes K2_BLOCKS blocks, 4 lanes each, the
@@ -539,6 +630,50 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
   const uint32_t sh = 64 - p;
+  if constexpr (K2_WIN2 && std::is_same<LP, const lds_u16*>::value) {
+    // LDS LUT (maxBits <= 11, a group reads <= 88 bits): 24-byte windows
+    // two groups ahead.  The window loaded when group g ends (ending at the
+    // byte of pos_{g+1}) covers groups g+1 and g+2, so group g+2 reads it and
+    // a load has a whole group more to land.  Both groups of a trip run on
+    // every lane; a lane that stops keeps its position (the tail redoes an
+    // absent-node group with the exact checks) and stores into the slack.
+    const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-24);
+    Win6 wa = win6_load(bs, m, pos);
+    asm volatile("" ::: "memory");
+    *(g_u64a1*)dummy = 0;
+    Win6 wb = win6_load(bs, m, pos);
+    asm volatile("" ::: "memory");
+    *(g_u64a1*)dummy = 0;
+    bool live = pos >= K2_GROUP * LUT_MAX_BITS && count + K2_GROUP <= cap;
+    auto group = [&](Win6& w) {
+      uint64_t acc = 0;
+      uint32_t used = 0, bad = 0;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        uint64_t t = win6_top64(w, pos - (int32_t)used);
+#pragma unroll
+        for (int j = 0; j < K2_GROUP / 2; j++) {
+          const uint32_t e = lut[(uint32_t)(t >> sh)];
+          const uint32_t nb = (e >> 8) & 0x7F;
+          bad |= e & LUT_ABSENT;
+          t <<= nb;
+          used += nb;
+          acc |= (uint64_t)(e & 0xFF) << (8 * (h * (K2_GROUP / 2) + j));
+        }
+      }
+      const bool ok = live && !bad;
+      pos = ok ? pos - (int32_t)used : pos;
+      w = win6_load(bs, m, pos);
+      asm volatile("" ::: "memory");
+      *(g_u64a1*)(ok ? out + count : dummy) = acc;
+      count += ok ? K2_GROUP : 0;
+      live = ok && pos >= K2_GROUP * LUT_MAX_BITS && count + K2_GROUP <= cap;
+    };
+    while (live) {
+      group(wa);
+      group(wb);
+    }
+  } else {
   // The next group's window is loaded before this group's store: vmcnt
   // drains in issue order, so a group waits for its window, not the store.
   // The loop entry repeats that order (a store into the block's literal
@@ -568,6 +703,7 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
     asm volatile("" ::: "memory");
     *(g_u64a1*)(out + count) = acc;
     count += K2_GROUP;
+  }
   }
   int st = 0;
   while (pos > 0 && !st) {
@@ -722,39 +858,6 @@ constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
 static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
 
-// 128-bit window of a backward bitstream: bits [wb, wb + 128) of the stream
-// (bit 0 = LSB of byte 0), loaded unaligned as the 16 bytes ending at the
-// byte that holds bit pos - 1, clamped at the input base.
-typedef uint32_t u32x4ua __attribute__((ext_vector_type(4), aligned(1)));
-typedef __attribute__((address_space(1))) const u32x4ua g_u32x4ua;
-struct Win4 {
-  uint32_t w0, w1, w2, w3;
-  int32_t wb;
-};
-// m = base - s (<= 0): the lowest byte offset the window may start at.
-__device__ inline Win4 win4_load(const uint8_t* s, int32_t m, int32_t pos) {
-  const int32_t tb = (pos + 7) >> 3;
-  const int32_t o = max(tb - 16, m);
-  const u32x4ua v = *(g_u32x4ua*)(s + o);
-  Win4 w;
-  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w;
-  w.wb = o * 8;
-  return w;
-}
-// The S bits [p - S, p) of the stream, S <= 32, MSB-first value; requires
-// wb <= p - S and p <= wb + 128 (else garbage, never a memory access).
-__device__ inline uint32_t win4_bits(const Win4& w, int32_t p, uint32_t S) {
-  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
-  const uint32_t k = y >> 5;
-  uint32_t lo = k == 0 ? w.w0 : w.w1;
-  uint32_t hi = k == 0 ? w.w1 : w.w2;
-  lo = k >= 2 ? w.w2 : lo;
-  hi = k >= 2 ? w.w3 : hi;
-  lo = k >= 3 ? w.w3 : lo;
-  hi = k >= 3 ? 0u : hi;
-  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
-}
-
 __device__ inline void k3_store(uint64_t* p, uint32_t pos, uint32_t states) {
   const uint64_t v = (uint64_t)pos | ((uint64_t)states << 32);
 #ifdef ZD_K3_NT_STORE
@@ -830,42 +933,6 @@ __device__ int seq_chain(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP
     if (st != 0 || last) break;
   }
   return st;
-}
-
-// The same chain with the bitstream window loaded two steps ahead: a
-// 24-byte window ending at the byte of pos_{i+1} covers every bit steps
-// i+1 and i+2 read (each step reads at most 63 extra + 27 state bits), so a
-// window load has a whole step more to land.
-struct Win6 {
-  uint32_t w0, w1, w2, w3, w4, w5;
-  int32_t wb;
-};
-typedef uint32_t u32x2ua __attribute__((ext_vector_type(2), aligned(1)));
-typedef __attribute__((address_space(1))) const u32x2ua g_u32x2ua;
-__device__ inline Win6 win6_load(const uint8_t* s, int32_t m, int32_t pos) {
-  const int32_t tb = (pos + 7) >> 3;
-  const int32_t o = max(tb - 24, m);
-  const u32x4ua v = *(g_u32x4ua*)(s + o);
-  const u32x2ua u = *(g_u32x2ua*)(s + o + 16);
-  Win6 w;
-  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w; w.w4 = u.x; w.w5 = u.y;
-  w.wb = o * 8;
-  return w;
-}
-__device__ inline uint32_t win6_bits(const Win6& w, int32_t p, uint32_t S) {
-  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
-  const uint32_t k = y >> 5;
-  uint32_t lo = k == 0 ? w.w0 : w.w1;
-  uint32_t hi = k == 0 ? w.w1 : w.w2;
-  lo = k >= 2 ? w.w2 : lo;
-  hi = k >= 2 ? w.w3 : hi;
-  lo = k >= 3 ? w.w3 : lo;
-  hi = k >= 3 ? w.w4 : hi;
-  lo = k >= 4 ? w.w4 : lo;
-  hi = k >= 4 ? w.w5 : hi;
-  lo = k >= 5 ? w.w5 : lo;
-  hi = k >= 5 ? 0u : hi;
-  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
 }
 
 template <typename TP, bool K3_SYM>
