@@ -64,6 +64,21 @@ int main() {
       }
     }
   }
+  // K3 fast-chain entries: nextState, extra + state bit count, 63 for a code above the maximum
+  for (int k = 0; k < 3; k++) {
+    for (int al = 5; al <= 9; al++) {
+      for (uint32_t c = 0; c < 64; c++) {
+        for (uint32_t ns = 1; ns < (2u << al); ns += 13) {
+          uint32_t e = k3f_entry(fse_entry(c, ns), k, al);
+          uint32_t bits = k == 0 ? (c < 36 ? LL_BITS[c] : 0) : (k == 2 ? (c < 53 ? ML_BITS[c] : 0) : c);
+          bool bad = k == 0 ? c > 35 : (k == 2 ? c > 52 : c > 31);
+          int nb = al - (31 - __builtin_clz(ns));
+          CHECK((e & 1023) == ns, "k3f ns");
+          CHECK(bad ? (e >> 10) == 63 : (e >> 10) == bits + nb, "k3f count k=%d al=%d c=%u ns=%u", k, al, c, ns);
+        }
+      }
+    }
+  }
   // direct records round trip (offset values past DIRECT_GIANT saturate)
   std::mt19937_64 g(7);
   for (int i = 0; i < 100000; i++) {

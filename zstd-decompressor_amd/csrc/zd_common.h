@@ -80,6 +80,20 @@ ZD_HD inline uint32_t k3_entry(uint32_t e, int k) {
   else { eb = c; bad = c > 31; }
   return ns | ((eb & 31) << 10) | (bad ? K3_BAD : 0u);
 }
+// K3's fast chain (zd_kernels.hip seq_chainf) reads one number per table per
+// step: nextState | (extra-bit count + state-bit count) << 10, with the
+// count 63 (never reached: <= 31 + 9) marking a code above the maximum.
+constexpr uint32_t K3F_BAD = 63u << 10;
+ZD_HD inline uint32_t k3f_entry(uint32_t e, int k, int al) {
+  const uint32_t c = e & 63, ns = (e >> 6) & 1023;
+  uint32_t base, eb;
+  bool bad;
+  if (k == 0) { ll_code(c, &base, &eb); bad = c > 35; }
+  else if (k == 2) { ml_code(c, &base, &eb); bad = c > 52; }
+  else { eb = c; bad = c > 31; }
+  const uint32_t nb = (uint32_t)(al - hb32(ns));
+  return ns | (bad ? K3F_BAD : (eb + nb) << 10);
+}
 
 // ---------------------------------------------------------------------------
 // Sequence records (K3 -> K4), 8 bytes each:

@@ -854,6 +854,11 @@ constexpr int K3_LANES = ZD_K3_LANES;
 #else
 #define K3_CHAIN seq_chain2      // window two steps ahead (default: 23.8 -> 18.3 ms on C4)
 #endif
+#ifdef ZD_K3_EXACT
+#define K3_ENTRY(e, k, al) k3_entry(e, k)       // experiment: checks inside the chain (seq_chain2 on LDS)
+#else
+#define K3_ENTRY(e, k, al) k3f_entry(e, k, al)  // default: seq_chainf, exact chain from HBM on a reject
+#endif
 constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
 static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
@@ -1104,6 +1109,97 @@ __device__ int seq_chain3(const uint8_t* bs, uint32_t bs_size, uintptr_t base, T
   return st;
 }
 
+// 32 bits of a 24-byte window from bit y up (y <= 192; bits past the window read as zero).
+__device__ inline uint32_t win6_at(const Win6& w, uint32_t y) {
+  const uint32_t k = y >> 5;
+  uint32_t lo = k == 0 ? w.w0 : w.w1;
+  uint32_t hi = k == 0 ? w.w1 : w.w2;
+  lo = k >= 2 ? w.w2 : lo;
+  hi = k >= 2 ? w.w3 : hi;
+  lo = k >= 3 ? w.w3 : lo;
+  hi = k >= 3 ? w.w4 : hi;
+  lo = k >= 4 ? w.w4 : lo;
+  hi = k >= 4 ? w.w5 : hi;
+  lo = k >= 5 ? w.w5 : lo;
+  hi = k >= 5 ? 0u : hi;
+  return __builtin_amdgcn_alignbit(hi, lo, y & 31);
+}
+
+// The fast chain: no checks inside the loop.  Each table gives nextState and
+// the step's total bit count for that table (k3f_entry), so a step is
+// pos -= tLL + tML + tOF, then the LL | ML | OF state bits are the low bits
+// at the new position.  Steps 0 .. n-2 update the states (a lane whose count
+// is odd runs step n-1 too, storing into the spare slot); the epilogue
+// re-reads record n-1 and checks the last step (extra bits only,
+// sequences.rs:223-229).  Anything the reference would reject -- a code
+// above the maximum anywhere (K3F_BAD), the position going negative before
+// the last step, or the last step's extra bits running out -- and the block
+// is decoded again by the exact chain, which finds the reference's error.
+// Returns 1 when the block needs the exact chain, else 0.
+__device__ int seq_chainf(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tll,
+                          const lds_u16* tml, const lds_u16* tof, int all, int alo, int alm, uint32_t n,
+                          uint64_t* __restrict__ out) {
+  if (bs_size == 0) return 1;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return 1;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
+  const int32_t A = all + alo + alm;
+  if (A > pos) return 1;
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-24);
+  const int32_t pos0 = pos;
+  const Win6 wi = win6_load(bs, m, pos);
+  const uint32_t v0 = win6_bits(wi, pos, (uint32_t)A);
+  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
+  pos -= A;
+  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
+  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
+  // Two records per 16-byte store, after both steps' window loads; the loop
+  // entry repeats that order (window, window, store).
+  typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(8)));
+  const uint64_t r0 = (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
+  Win6 wa = win6_load(bs, m, pos0);
+  Win6 wb = win6_load(bs, m, pos);
+  asm volatile("" ::: "memory");
+  *(u64x2u*)out = u64x2u{r0, r0};                 // slot 1: rewritten by the loop, or the spare
+  uint32_t mx = 0;
+  auto step = [&](Win6& use) -> uint64_t {
+    const uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
+    mx = max(mx, max(eLL, max(eML, eOF)));
+    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
+    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
+    pos -= (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10));
+    const uint32_t r = win6_at(use, (uint32_t)(pos - use.wb));
+#if defined(ZD_EXP_NOLOAD)
+    use.wb = pos - 100;                            // experiment: stale window bits, no load
+#else
+    use = win6_load(bs, m, pos);                   // for the step after next
+#endif
+    const uint32_t vO = __builtin_amdgcn_ubfe(r, 0, nbO), vM = __builtin_amdgcn_ubfe(r, nbO, nbM);
+    const uint32_t vL = __builtin_amdgcn_ubfe(r, nbO + nbM, nbL);
+    sLL = (nsL << nbL) + vL - TL;
+    sML = (nsM << nbM) + vM - TM;
+    sOF = (nsO << nbO) + vO - TO;
+    return (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
+  };
+  for (uint32_t i = 0; i + 1 < n; i += 2) {
+    const uint64_t ra = step(wa);
+    const uint64_t rb = step(wb);                  // slot n when n - 1 is odd: the spare
+    asm volatile("" ::: "memory");
+#ifndef ZD_EXP_NOSTORE
+    *(u64x2u*)(out + i + 1) = u64x2u{ra, rb};
+#endif
+  }
+  // the last step: its extra bits only
+  const uint64_t rl = *(volatile uint64_t*)(out + n - 1);
+  const int32_t pl = (int32_t)(uint32_t)rl;
+  const uint32_t st = (uint32_t)(rl >> 32);
+  const uint32_t eLL = tll[st & 1023], eML = tml[(st >> 10) & 1023], eOF = tof[(st >> 20) & 1023];
+  mx = max(mx, max(eLL, max(eML, eOF)));
+  const uint32_t S = (__builtin_clz(eLL & 1023) + aL) + (__builtin_clz(eML & 1023) + aM) + (__builtin_clz(eOF & 1023) + aO);
+  const int32_t E = (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10) - S);
+  return (mx >= K3F_BAD || pl < 0 || E > pl) ? 1 : 0;
+}
+
 __device__ inline void k3_fail(const CompBlock& C, uint32_t ci, CompState* cstate, FrameState* fstate, int st) {
   key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
   cstate[ci].stop = 1;
@@ -1151,14 +1247,14 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
         l_u4* d4 = (l_u4*)(mine + dst[k]);
         for (int e = 0; e < cnt / 8; e++) {
           u32x4 v = s4[e];
-          v.x = k3_entry(v.x & 0xFFFF, k) | (k3_entry(v.x >> 16, k) << 16);
-          v.y = k3_entry(v.y & 0xFFFF, k) | (k3_entry(v.y >> 16, k) << 16);
-          v.z = k3_entry(v.z & 0xFFFF, k) | (k3_entry(v.z >> 16, k) << 16);
-          v.w = k3_entry(v.w & 0xFFFF, k) | (k3_entry(v.w >> 16, k) << 16);
+          v.x = K3_ENTRY(v.x & 0xFFFF, k, al[k]) | (K3_ENTRY(v.x >> 16, k, al[k]) << 16);
+          v.y = K3_ENTRY(v.y & 0xFFFF, k, al[k]) | (K3_ENTRY(v.y >> 16, k, al[k]) << 16);
+          v.z = K3_ENTRY(v.z & 0xFFFF, k, al[k]) | (K3_ENTRY(v.z >> 16, k, al[k]) << 16);
+          v.w = K3_ENTRY(v.w & 0xFFFF, k, al[k]) | (K3_ENTRY(v.w >> 16, k, al[k]) << 16);
           d4[e] = v;
         }
       } else {
-        for (int e = 0; e < cnt; e++) mine[dst[k] + e] = (uint16_t)k3_entry(((g_u16*)g[k])[e], k);
+        for (int e = 0; e < cnt; e++) mine[dst[k] + e] = (uint16_t)K3_ENTRY(((g_u16*)g[k])[e], k, al[k]);
       }
     }
   }
@@ -1167,11 +1263,22 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
   const CompState cs = cstate[ci];
   const uint8_t* blk = src + C.src;
   const uintptr_t lo = (uintptr_t)src;
-  int st;
+  int st = 0;
+#ifdef ZD_K3_EXACT
   if (use_lds)
     st = K3_CHAIN<const lds_u16*, false>(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM,
                                           al[0], al[1], al[2], C.nseq, recs + C.seq_out);
   else
+#else
+  bool exact = !use_lds;
+  if (use_lds)
+    exact = seq_chainf(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM, al[0], al[1],
+                       al[2], C.nseq, recs + C.seq_out) != 0;
+#if defined(ZD_EXP_NOLOAD) || defined(ZD_EXP_NOSTORE)
+  exact = !use_lds;                               // experiments: garbage chains, no reruns
+#endif
+  if (exact)
+#endif
     st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0],
                                  al[1], al[2], C.nseq, recs + C.seq_out);
   if (st) k3_fail(C, ci, cstate, fstate, st);
