@@ -413,7 +413,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
         }
         cb.seq_out = nrec;
         nseq_total += cb.nseq;
-        nrec += cb.nseq + (cb.nseq ? 1 : 0);     // K3 writes one spare record past the block's last
+        nrec += cb.nseq + (cb.nseq ? 2 : 0);     // K3 writes up to two spare records past the block's last
         seqs_in_frame |= cb.nseq > 0;
         P->comps.push_back(cb);
         br.comp = (int32_t)ci;

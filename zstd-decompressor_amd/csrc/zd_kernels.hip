@@ -854,6 +854,17 @@ constexpr int K3_LANES = ZD_K3_LANES;
 #else
 #define K3_CHAIN seq_chain2      // window two steps ahead (default: 23.8 -> 18.3 ms on C4)
 #endif
+#ifndef ZD_K3_LA
+#define ZD_K3_LA 4                   // windows L steps ahead (C4: L2 17.3 ms, L3 14.5, L4 13.8)
+#endif
+#ifndef ZD_K3_WN
+#define ZD_K3_WN 6                   // window dwords
+#endif
+#if ZD_K3_LA == 2
+#define K3_FAST seq_chainf
+#else
+#define K3_FAST seq_chainfl<ZD_K3_LA, ZD_K3_WN>
+#endif
 #ifdef ZD_K3_EXACT
 #define K3_ENTRY(e, k, al) k3_entry(e, k)       // experiment: checks inside the chain (seq_chain2 on LDS)
 #else
@@ -1200,6 +1211,131 @@ __device__ int seq_chainf(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   return (mx >= K3F_BAD || pl < 0 || E > pl) ? 1 : 0;
 }
 
+// N-dword bitstream window ending at the byte of pos (clamped to start at m).
+template <int N>
+struct WinN {
+  uint32_t w[N];
+  int32_t wb;
+};
+template <int N>
+__device__ inline WinN<N> winn_load(const uint8_t* s, int32_t m, int32_t pos) {
+  const int32_t o = max(((pos + 7) >> 3) - 4 * N, m);
+  WinN<N> w;
+#pragma unroll
+  for (int k = 0; k + 4 <= N; k += 4) {
+    const u32x4ua v = *(g_u32x4ua*)(s + o + 4 * k);
+    w.w[k] = v.x; w.w[k + 1] = v.y; w.w[k + 2] = v.z; w.w[k + 3] = v.w;
+  }
+  if (N % 4 == 2) {
+    const u32x2ua u = *(g_u32x2ua*)(s + o + 4 * (N - 2));
+    w.w[N - 2] = u.x; w.w[N - 1] = u.y;
+  }
+  w.wb = o * 8;
+  return w;
+}
+// 32 bits from bit y up (0 <= y <= 32 N; bits past the window read as zero)
+template <int N>
+__device__ inline uint32_t winn_at(const WinN<N>& w, uint32_t y) {
+  const uint32_t k = y >> 5;
+  uint32_t lo = w.w[0], hi = w.w[1];
+#pragma unroll
+  for (int i = 1; i < N; i++) {
+    lo = k >= (uint32_t)i ? w.w[i] : lo;
+    hi = k >= (uint32_t)i ? (i + 1 < N ? w.w[i + 1] : 0u) : hi;
+  }
+  return __builtin_amdgcn_alignbit(hi, lo, y & 31);
+}
+
+// seq_chainf with windows loaded L steps ahead (a ring of L windows).  A
+// 24-byte window ending at the byte of pos_{i+1} covers steps i+1..i+L when
+// they read <= 185 bits together (text: ~35 bits a step); a lane whose steps
+// read more sees a window start above its position (ymin < 0) and the block
+// goes to the exact chain.  U steps per trip, records stored in pairs; a pair
+// past the block's last record goes to its two spare slots (host: seq_out).
+template <int L, int N>
+__device__ int seq_chainfl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tll,
+                           const lds_u16* tml, const lds_u16* tof, int all, int alo, int alm, uint32_t n,
+                           uint64_t* __restrict__ out) {
+  constexpr int U = (L % 2 == 0) ? L : 2 * L;
+  static_assert(N % 4 == 0 || N % 4 == 2, "window: dwordx4 pieces and one dwordx2");
+  if (bs_size == 0) return 1;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return 1;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
+  const int32_t A = all + alo + alm;
+  if (A > pos) return 1;
+  // windows never start below the input nor end past the stream's block
+  if ((intptr_t)bs - (intptr_t)base + (intptr_t)bs_size < 4 * N) return 1;
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)(-4 * N));
+  const int32_t pos0 = pos;
+  const Win6 wi = win6_load(bs, m, pos);
+  const uint32_t v0 = win6_bits(wi, pos, (uint32_t)A);
+  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
+  pos -= A;
+  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
+  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
+  typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(8)));
+  const uint64_t r0 = (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
+  // loop entry: the trip's memory-op order (window, window, store, ...)
+  WinN<N> w[L];
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    w[k] = winn_load<N>(bs, m, k == 0 ? pos0 : pos);
+    if (k & 1) {
+      asm volatile("" ::: "memory");
+      *(u64x2u*)out = u64x2u{r0, r0};
+    }
+  }
+  if (L & 1) {
+    asm volatile("" ::: "memory");
+    *(u64x2u*)out = u64x2u{r0, r0};
+  }
+  uint32_t mx = 0;
+  int32_t ymin = 0;
+  auto step = [&](WinN<N>& use) -> uint64_t {
+    const uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
+    mx = max(mx, max(eLL, max(eML, eOF)));
+    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
+    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
+    pos -= (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10));
+    const int32_t y = pos - use.wb;
+    ymin = min(ymin, y);
+    const uint32_t r = winn_at<N>(use, (uint32_t)y);
+#if defined(ZD_EXP_NOLOAD)
+    use.wb = pos - 100;                            // experiment: stale window bits, no load
+#else
+    use = winn_load<N>(bs, m, pos);                // for the step L on
+#endif
+    const uint32_t vO = __builtin_amdgcn_ubfe(r, 0, nbO), vM = __builtin_amdgcn_ubfe(r, nbO, nbM);
+    const uint32_t vL = __builtin_amdgcn_ubfe(r, nbO + nbM, nbL);
+    sLL = (nsL << nbL) + vL - TL;
+    sML = (nsM << nbM) + vM - TM;
+    sOF = (nsO << nbO) + vO - TO;
+    return (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
+  };
+  for (uint32_t i = 0; i + 1 < n; i += U) {
+#pragma unroll
+    for (int k = 0; k < U; k += 2) {
+      const uint64_t qa = step(w[k % L]);
+      const uint64_t qb = step(w[(k + 1) % L]);
+      asm volatile("" ::: "memory");
+      const uint32_t slot = i + 1 + k;
+      *(u64x2u*)(out + (slot < n ? slot : n)) = u64x2u{qa, qb};
+    }
+  }
+  const uint64_t rl = *(volatile uint64_t*)(out + n - 1);
+  const int32_t pl = (int32_t)(uint32_t)rl;
+  const uint32_t st = (uint32_t)(rl >> 32);
+  const uint32_t eLL = tll[st & 1023], eML = tml[(st >> 10) & 1023], eOF = tof[(st >> 20) & 1023];
+  mx = max(mx, max(eLL, max(eML, eOF)));
+  const uint32_t S = (__builtin_clz(eLL & 1023) + aL) + (__builtin_clz(eML & 1023) + aM) + (__builtin_clz(eOF & 1023) + aO);
+  const int32_t E = (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10) - S);
+#if defined(ZD_EXP_NOLOAD)
+  ymin = 0;
+#endif
+  return (mx >= K3F_BAD || ymin < 0 || pl < 0 || E > pl) ? 1 : 0;
+}
+
 __device__ inline void k3_fail(const CompBlock& C, uint32_t ci, CompState* cstate, FrameState* fstate, int st) {
   key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_SEQUENCES, 0, st));
   cstate[ci].stop = 1;
@@ -1272,7 +1408,7 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
 #else
   bool exact = !use_lds;
   if (use_lds)
-    exact = seq_chainf(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM, al[0], al[1],
+    exact = K3_FAST(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM, al[0], al[1],
                        al[2], C.nseq, recs + C.seq_out) != 0;
 #if defined(ZD_EXP_NOLOAD) || defined(ZD_EXP_NOSTORE)
   exact = !use_lds;                               // experiments: garbage chains, no reruns
