@@ -1701,7 +1701,10 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   uint64_t err_key = KEY_NONE;
   // HBM holds [0, fl_safe) with every store completed (the bytes two batches
   // back); fl_last = the flush boundary after the previous batch
-  int32_t fl_safe = X.fl, fl_last = X.fl;
+  int32_t fl_safe = X.fl;
+#ifdef ZD_K4_LATE_FLUSH
+  int32_t fl_last = X.fl;
+#endif
 #ifdef ZD_K4_PROF
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime(), nb = 0, nr = 0;
 #define K4P(i) do { const uint64_t tn = __builtin_amdgcn_s_memtime(); ph[i] += tn - tq; tq = tn; } while (0)
@@ -1776,6 +1779,20 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const bool valid = i < n;
         K4P(7);
         *(l_u32x4*)(stg + 16 * lane) = litA;         // this batch's literal bytes from the cursor on
+#ifndef ZD_K4_LATE_FLUSH
+        // The previous batch's output goes to HBM here, after the wait for
+        // this batch's prefetched loads: those stores then have a batch to
+        // drain before the next wait (vmcnt counts stores too, in order).
+        // (the wait below is the one the compiler places here anyway)
+        wait_vm();
+        fl_safe = X.fl;
+#endif
+        // the next batch's windows and the records after it, first thing
+        const WinU winB = win_of(recB, s0 + 64 + lane < n);
+        const uint64_t recC = rec_at(s0 + 128 + lane);
+#ifndef ZD_K4_LATE_FLUSH
+        k4_flush(X, false);
+#endif
         // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
         // K3 recorded the bit position and the three states; OF, ML, LL
         // extra bits are read here, in that order, below the position.
@@ -1799,13 +1816,13 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           }
         }
         K4P(0);
-        // the next batch's windows, the records after it
-        const WinU winB = win_of(recB, s0 + 64 + lane < n);
-        const uint64_t recC = rec_at(s0 + 128 + lane);
+        // the next batch's literal bytes (used only when all 64 lanes
+        // execute, so from the cursor after all of them)
+        const uint32_t inc_ll = wave_scan_incl(ll);
+        const u32x4 litB = lit_of(lit_cursor + (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, 63));
         k4_room(X);
         const uint32_t tot = ll + ml;
         const uint32_t inc_tot = wave_scan_incl(tot);
-        const uint32_t inc_ll = wave_scan_incl(ll);
         const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
         const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= (int64_t)X.space() - 16);
         const uint32_t k = (uint32_t)__popcll(fitm);
@@ -1885,8 +1902,6 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
         const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
         if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN); break; }
-        // the next batch's literal bytes
-        const u32x4 litB = lit_of(lit_cursor + L);
         const bool act = (uint32_t)lane < k;
         k4_sync();                               // staged literals visible
         // literals (every lane its own run; from the stage when it holds them)
@@ -1906,7 +1921,18 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           l_u8* d = X.at(q);
           sts_n(d, fv0, ml);
           if (ml > 16) sts_n(d + 16, fv1, ml - 16);
-          for (uint32_t x = 32; x < ml; x += 16) sts_n(d + x, ldg16_nt(X.out + slo + x), ml - x);
+          // the rest four pieces at a time: one load latency per 64 bytes
+          for (uint32_t x = 32; x < ml; x += 64) {
+            u32x4 v1 = fv0, v2 = fv0, v3 = fv0;
+            const u32x4 v0 = ldg16_nt(X.out + slo + x);
+            if (x + 16 < ml) v1 = ldg16_nt(X.out + slo + x + 16);
+            if (x + 32 < ml) v2 = ldg16_nt(X.out + slo + x + 32);
+            if (x + 48 < ml) v3 = ldg16_nt(X.out + slo + x + 48);
+            sts_n(d + x, v0, ml - x);
+            if (x + 16 < ml) sts_n(d + x + 16, v1, ml - x - 16);
+            if (x + 32 < ml) sts_n(d + x + 32, v2, ml - x - 32);
+            if (x + 48 < ml) sts_n(d + x + 48, v3, ml - x - 48);
+          }
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
         uint64_t done = __ballot(!act || ml == 0 || far);
@@ -1945,13 +1971,18 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         lit_cursor += L;
         X.pos += (int32_t)T;
         s0 += k;
+#ifdef ZD_K4_LATE_FLUSH
         fl_safe = fl_last;
         fl_last = X.fl;
         k4_flush(X, false);
+#endif
         K4P(5);
         if (k < 64 || s0 >= n) break;                  // a partial batch: the pipeline restarts at s0
         recA = recB; winA = winB; recB = recC; litA = litB;
       }
+#ifndef ZD_K4_LATE_FLUSH
+      k4_flush(X, false);                            // k4_room and the large-sequence path expect it
+#endif
       if (big && err_key == KEY_NONE) {
         // one sequence larger than the window's room: the whole wave copies it
         if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, bll) ||
