@@ -179,3 +179,63 @@ def test_many_frame_roundtrip_large():
     data = gen.frames(src, 128 << 10, 3)
     from zstd_decompressor import decompress
     assert decompress(data) == src
+
+
+def _ncount(al, probs):
+    """FSE table description (the inverse of parse_fse_table, fse.rs:16-69):
+    probabilities of symbols 0.. (-1 = "less than one"), LSB-first bits."""
+    bits, nbits = 0, 0
+
+    def put(v, n):
+        nonlocal bits, nbits
+        bits |= v << nbits
+        nbits += n
+    put(al - 5, 4)
+    remaining, i = 1 << al, 0
+    while remaining > 0:
+        d = probs[i] + 1
+        nb = (remaining + 1).bit_length()                   # highbit(remaining + 1) + 1
+        low = (1 << (nb - 1)) - 1
+        thr = (1 << nb) - 1 - (remaining + 1)
+        if d < thr:
+            put(d, nb - 1)
+        elif d <= low:
+            put(d, nb)
+        else:
+            put(d + thr, nb)
+        remaining -= abs(probs[i])
+        i += 1
+        if probs[i - 1] == 0:                               # repeat flags for the zeros that follow
+            z = 0
+            while i + z < len(probs) and probs[i + z] == 0:
+                z += 1
+            i += z
+            while True:
+                put(min(z, 3), 2)
+                if z < 3:
+                    break
+                z -= 3
+    assert i == len(probs), (i, len(probs))
+    return bits.to_bytes((nbits + 7) // 8, "little")
+
+
+def test_k1_large_tables():
+    """Sequence tables with more than 64 symbols (LL codes past the maximum):
+    K1's first pass flags the block and the large-scratch pass builds it
+    (zd_kernels.hip zd_k_tables<true>); status and output match the oracle."""
+    r = random.Random(77)
+    for nsym, al in ((70, 6), (65, 7), (100, 7), (255, 8)):
+        probs = [1] * (nsym - 1) + [(1 << al) - (nsym - 1)]   # the last symbol takes the rest
+        if probs[-1] <= 0:
+            probs = [1] * ((1 << al) - 1) + [0] * (nsym - (1 << al)) + [1]
+        assert sum(abs(p) for p in probs) == 1 << al and len(probs) == nsym
+        table = _ncount(al, probs)
+        for trial in range(6):
+            bitstream = bytes(r.randrange(256) for _ in range(r.randrange(3, 12))) + bytes([r.randrange(1, 256)])
+            nseq = r.choice([1, 2, 5])
+            seqs = bytes([nseq, 0x80]) + table + bitstream       # LL FSE, OF/ML predefined
+            lits = bytes([(3 << 3) | 0]) + b"xyz"               # raw literals, 3 bytes
+            content = lits + seqs
+            hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
+            frame = b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x00]) + hdr + content
+            assert_parity(frame, False, f"nsym {nsym} al {al} trial {trial}", allow_ood=True)

@@ -286,6 +286,7 @@ struct CompState {
   uint32_t stop;           // nonzero: literals/sequences stage failed or is out of domain
   uint8_t al[3];           // accuracy log of the LL/OF/ML table in this block's FSE slot
   uint8_t huf_bits;        // maxBits of this block's LUT
+  uint32_t k1_big;         // K1: tables need the large scratch (second pass)
 };
 
 // Blocks of frames in order (all types).

@@ -138,8 +138,13 @@ struct FwBits {
   __device__ inline uint32_t bytes_read() const { return pos / 8 + (pos % 8 > 0); }
 };
 
-// parse_fse_table (fse.rs:16-69)
-__device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t* nsym_out) {
+// A table needs K1's large scratch (more than K1S_SYMS symbols, or a
+// Huffman-weight table deeper than AL 6): the block goes to the second pass.
+constexpr int K1_BIG = 1;
+constexpr uint32_t K1S_SYMS = 64;
+
+// parse_fse_table (fse.rs:16-69); dist holds max_sym entries (256: all)
+__device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t* nsym_out, uint32_t max_sym) {
   uint32_t v;
   if (int r = in.take(4, &v)) return r;
   int al = (int)v + 5;
@@ -165,13 +170,15 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
     }
     int32_t proba = decoded - 1;
     remaining -= proba < 0 ? -proba : proba;
-    if (n_sym < 256) dist[n_sym] = (int16_t)proba;
+    if (n_sym < max_sym) dist[n_sym] = (int16_t)proba;
+    else if (max_sym < 256) return K1_BIG;
     n_sym++;
     if (proba == 0) {
       for (;;) {
         if (int r = in.take(2, &v)) return r;
         for (uint32_t z = 0; z < v; z++) {
-          if (n_sym < 256) dist[n_sym] = 0;
+          if (n_sym < max_sym) dist[n_sym] = 0;
+          else if (max_sym < 256) return K1_BIG;
           n_sym++;
         }
         if (v != 3) break;
@@ -228,12 +235,25 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* t
 constexpr int K1_LANES = 16;
 constexpr int K1_MAX_WEIGHTS = 255;               // a Huffman tree of 256 symbols (RFC 8878 4.2.1)
 struct K1Lane {
+  static constexpr uint32_t SYMS = 256, WFSE = FSE_TAB;
   uint16_t fse[FSE_TAB];                          // Huffman-weight FSE table
   uint8_t sym[FSE_TAB];                           // spread scratch
   uint16_t next[256];
   int16_t dist[256];
   uint8_t weights[K1_MAX_WEIGHTS + 1];
   uint16_t cnt[16], start[16], placed[16];        // per code width (<= 12)
+};
+// The first pass's scratch (1.2 KiB instead of 2.9: eight workgroups per CU
+// instead of three, so table builds hide each other's LDS latency): up to 64
+// symbols per table and Huffman-weight tables of AL <= 6 (zstd's limit).
+struct K1LaneS {
+  static constexpr uint32_t SYMS = K1S_SYMS, WFSE = 64;
+  uint16_t fse[64];
+  uint8_t sym[FSE_TAB];
+  uint16_t next[K1S_SYMS];
+  int16_t dist[K1S_SYMS];
+  uint8_t weights[K1_MAX_WEIGHTS + 1];
+  uint16_t cnt[16], start[16], placed[16];
 };
 
 // Entries [a, b) that no code reaches: the tree node there is Absent.  Its
@@ -256,7 +276,8 @@ __device__ void lut_holes(uint16_t* lut, int p, uint32_t a, uint32_t b) {
 // 80-203) -> LUT of 2^p u16 entries {symbol | width << 8}; entries no code
 // reaches get LUT_ABSENT | depth of the absent tree node.  Returns status;
 // *p_out = maxBits.
-__device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, K1Lane& L,
+template <typename LN>
+__device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, LN& L,
                                uint16_t* lut, int* p_out) {
   int st = 0;
   uint32_t nw = 0;
@@ -266,7 +287,8 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
     FwBits fw{desc + 1, h, 0};
     uint8_t al;
     uint32_t nsym;
-    st = parse_ncount(fw, &al, L.dist, &nsym);
+    st = parse_ncount(fw, &al, L.dist, &nsym, LN::SYMS);
+    if (!st && (1u << al) > LN::WFSE) st = K1_BIG;
     if (!st) st = build_fse(al, L.dist, nsym, L.fse, L.sym, L.next);
     BwBits bs;
     if (!st) st = bs.init(desc + 1 + fw.bytes_read(), h - fw.bytes_read(), src, src_end);
@@ -380,7 +402,8 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
 // descriptions and predefined distributions, in LL, OF, ML order, each
 // written as compact entries to the block's slot.  Returns status; *stage_sub
 // = table index of a failure (3: the empty-bitstream check).
-__device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, K1Lane& L, uint16_t* slot, uint8_t al_out[3],
+template <typename LN>
+__device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, LN& L, uint16_t* slot, uint8_t al_out[3],
                                  uint32_t* bs_off, uint32_t* bs_size, int* sub) {
   uint32_t pos = C.seq_tables;
   for (int k = 0; k < 3; k++) {
@@ -397,7 +420,7 @@ __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, K1Lane&
         FwBits fw{blk + pos, C.size - pos, 0};
         uint8_t a;
         uint32_t nsym;
-        st = parse_ncount(fw, &a, L.dist, &nsym);
+        st = parse_ncount(fw, &a, L.dist, &nsym, LN::SYMS);
         if (!st) st = build_fse(a, L.dist, nsym, tab, L.sym, L.next);
         al = a;
         pos += fw.bytes_read();
@@ -418,21 +441,31 @@ __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, K1Lane&
   return pos >= C.size ? ZD_E_EMPTY_SLICE : 0;
 }
 
+// Two passes: every block with the small scratch (K1LaneS), then the blocks
+// that flagged k1_big with the large one (the same code; the first pass
+// records nothing for them).
+template <bool BIG>
 __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restrict__ src, uint64_t src_size,
                                                         const CompBlock* __restrict__ comp, CompState* cstate,
                                                         FrameState* fstate, const uint32_t* __restrict__ list,
                                                         uint32_t n_list, uint16_t* luts, uint16_t* fses) {
-  __shared__ K1Lane lanes[K1_LANES];
+  typedef typename std::conditional<BIG, K1Lane, K1LaneS>::type LN;
+  __shared__ LN lanes[K1_LANES];
   const uint32_t li = blockIdx.x * K1_LANES + threadIdx.x;
   if (li >= n_list) return;
-  K1Lane& L = lanes[threadIdx.x];
+  LN& L = lanes[threadIdx.x];
   const uint32_t ci = list[li];
+  if (BIG && !cstate[ci].k1_big) return;
   const CompBlock C = comp[ci];
   if (C.prebuilt) return;
   const uint8_t* blk = src + C.src;
   if (C.lit_type == LIT_COMPRESSED && C.host_stage > PS_HUF_DESC) {
     int p = 0;
     const int st = k1_huffman_lane(blk + C.lit_data, src, src + src_size, L, luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
+    if (!BIG && st == K1_BIG) {
+      cstate[ci].k1_big = 1;
+      return;
+    }
     if (st == ZD_E_OUT_OF_DOMAIN) {
       // the tree parsed (the reference's Block::parse goes on to the
       // sequences section) but no GPU LUT holds it: out of domain where the
@@ -451,6 +484,10 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
     uint32_t bo = 0, bsz = 0;
     int sub = 0;
     const int st = k1_sequences_lane(blk, C, L, fses + (uint64_t)C.fse_slot * FSE_SLOT, al, &bo, &bsz, &sub);
+    if (!BIG && st == K1_BIG) {
+      cstate[ci].k1_big = 1;
+      return;
+    }
     for (int k = 0; k < 3; k++)
       if (C.modes[k] != M_REPEAT && (sub > k || !st)) cstate[ci].al[k] = al[k];
     cstate[ci].bs_off = bo;
@@ -2558,9 +2595,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_rawcopy, dim3(a.n_copies), dim3(256), 0, s, a.src, a.out,
                        (const CopyDesc*)(ws + W.copies));
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
-  if (a.n_tables && (a.kmask & 1))
-    hipLaunchKernelGGL(zd_k_tables, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
+  if (a.n_tables && (a.kmask & 1)) {
+    hipLaunchKernelGGL(zd_k_tables<false>, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
                        a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
+    hipLaunchKernelGGL(zd_k_tables<true>, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
+                       a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
+  }
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   // K2 and K3 are independent once K1 is done: K2 runs on the aux stream
   // beside K3 (not when timing kernels one by one)
