@@ -642,7 +642,10 @@ __device__ inline uint64_t win6_top64(const Win6& w, int32_t q) {
 // each stream holds its RFC share.  A block whose tree is deeper than 11 bits
 // makes its workgroup read LUTs from HBM.
 // ---------------------------------------------------------------------------
-constexpr int K2_BLOCKS = 8;
+#ifndef ZD_K2_BLOCKS
+#define ZD_K2_BLOCKS 8
+#endif
+constexpr int K2_BLOCKS = ZD_K2_BLOCKS;
 constexpr int K2_LANES = 4 * K2_BLOCKS;
 constexpr int K2_LUT_BITS = 11;
 constexpr int K2_GROUP = 8;
