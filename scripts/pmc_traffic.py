@@ -17,10 +17,13 @@ def per_dispatch(d, counter):
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         if r["Counter_Name"] != counter:
             continue
-        k = r["Kernel_Name"].split("(")[0].replace("zd::", "")
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("zd::", "")
         agg[k] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
-    return {k: agg[k] / len(disp[k]) * 1024.0 for k in agg}
+    out = collections.defaultdict(float)
+    for k in agg:                                  # zd_k_tables<false> + <true>: one pass each
+        out[k.split("<")[0]] += agg[k] / len(disp[k]) * 1024.0
+    return dict(out)
 
 
 fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
