@@ -1508,7 +1508,14 @@ typedef __attribute__((address_space(3))) u32x4 l_u32x4;
 __device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
 // Match sources in HBM are read through the caches: the frame's own recent
 // output, re-read by later matches (nontemporal loads here: 28.3 -> 23.4 ms)
+#ifdef ZD_EXP_NOFAR
+// experiment: match sources "read" from the window instead of HBM (wrong bytes, timing only)
+__device__ inline u32x4 ldg16_nt(const uint8_t* p) {
+  return *(const __attribute__((address_space(3))) u32x4a1*)(((uintptr_t)p & 4095));
+}
+#else
 __device__ inline u32x4 ldg16_nt(const uint8_t* p) { return *(g_cu32x4a1*)p; }
+#endif
 // streams read once (records, literals): nontemporal, to leave the caches
 // to the frame outputs
 __device__ inline u32x4 ldg16_once(const uint8_t* p) {
@@ -1945,7 +1952,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const bool act = (uint32_t)lane < k;
         k4_sync();                               // staged literals visible
         // literals (every lane its own run; from the stage when it holds them)
+#ifdef ZD_EXP_NOLIT
+        if (false) {                              // experiment: no literal copies
+#else
         if (act && ll) {
+#endif
           l_u8* d = X.at(X.pos + (int32_t)opos);
           if (!lit_stage || lpos + ll <= 1024) {
             const l_u8* sp = (const l_u8*)stg + lpos;
@@ -1975,7 +1986,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           }
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
+#ifdef ZD_EXP_NOROUNDS
+        uint64_t done = ~0ull;                    // experiment: no near-match copies
+#else
         uint64_t done = __ballot(!act || ml == 0 || far);
+#endif
         k4_sync();
         K4P(3);
         while (done != ~0ull) {
