@@ -711,7 +711,17 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // K2 beside K3 on a second stream measured slower on C4 (61.4 vs 57.9 ms:
   // K3 is LDS-bound and K2 takes its CUs), so it is opt-in (ZD_FORK=1)
   static const bool fork = getenv("ZD_FORK") && atoi(getenv("ZD_FORK")) == 1;
-  if (!P->aux && fork) {
+  static const bool overlap = getenv("ZD_OVERLAP") && atoi(getenv("ZD_OVERLAP")) == 1;
+  if (overlap && !fork && P->fdesc.size() > 1) {
+    // K4 of the first half of the frames beside K3 of the second half
+    // (measured slower on C4, 45.1 vs 41.2 ms: both kernels are LDS-bound)
+    a.overlap = true;
+    a.n_frames_a = (uint32_t)(P->fdesc.size() / 2);
+    uint32_t k = 0;
+    while (k < P->list_seq.size() && P->comps[P->list_seq[k]].frame < a.n_frames_a) k++;
+    a.n_seq_a = k;
+  }
+  if (!P->aux && (fork || a.overlap)) {
     HIPCHK(hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&P->fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&P->join, hipEventDisableTiming));

@@ -1715,14 +1715,15 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                                                    const CompState* __restrict__ cstate,
                                                    const uint8_t* __restrict__ lits,
                                                    const uint64_t* __restrict__ seqs,
-                                                   const uint16_t* __restrict__ fses, uint32_t n_frames) {
+                                                   const uint16_t* __restrict__ fses, uint32_t f_begin,
+                                                   uint32_t f_end) {
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
   __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];      // a batch's literal bytes
   const int lane = threadIdx.x;
   // persistent over frames when the grid is capped
-  for (uint32_t f = blockIdx.x; f < n_frames; f += gridDim.x) {
+  for (uint32_t f = f_begin + blockIdx.x; f < f_end; f += gridDim.x) {
   const FrameDesc F = frames[f];
   if (F.lds) continue;                           // K4F executes this frame
   FrameState* S = &fstate[f];
@@ -2622,7 +2623,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   // K2 and K3 are independent once K1 is done: K2 runs on the aux stream
   // beside K3 (not when timing kernels one by one)
-  const bool fork = a.aux && !a.events && a.n_huf && a.n_seq && (a.kmask & 6) == 6;
+  const bool fork = a.aux && !a.overlap && !a.events && a.n_huf && a.n_seq && (a.kmask & 6) == 6;
   hipStream_t s2 = fork ? a.aux : s;
   if (fork) {
     if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
@@ -2634,17 +2635,38 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (fork)
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
-  if (a.n_seq && (a.kmask & 4))
-    hipLaunchKernelGGL(zd_k_sequences, dim3((a.n_seq + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
-                       cstate, fstate, (const uint32_t*)(ws + W.list_seq), a.n_seq, (const uint16_t*)fses,
-                       seqs);
-  if (fork)
+  auto k3 = [&](uint32_t l0, uint32_t l1) {
+    if (l1 > l0 && (a.kmask & 4))
+      hipLaunchKernelGGL(zd_k_sequences, dim3((l1 - l0 + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
+                         cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0, (const uint16_t*)fses,
+                         seqs);
+  };
+  auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st) {
+    const uint32_t n = f1 - f0;
+    if (n && a.n_frames > a.n_k4f && (a.kmask & 8))   // frames on the streaming K4 (K4F's exit at once)
+      hipLaunchKernelGGL(zd_k_execute, dim3(a.k4_grid && a.k4_grid < n ? a.k4_grid : n), dim3(64), 0, st, a.src,
+                         a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
+                         (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1);
+  };
+  // Overlap (opt-in, ZD_OVERLAP=1): K4 of the first frames on the aux
+  // stream beside K3 of the rest (their sequences come later in list_seq).
+  const bool overlap = a.aux && a.overlap && !a.events && !fork && a.n_frames_a && a.n_frames_a < a.n_frames;
+  if (overlap) {
+    k3(0, a.n_seq_a);
+    if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
+    k4(0, a.n_frames_a, a.aux);
+    if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
+    k3(a.n_seq_a, a.n_seq);
+    k4(a.n_frames_a, a.n_frames, s);
     if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-  if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
-  if (a.n_frames > a.n_k4f && (a.kmask & 8))     // frames on the streaming K4 (the rest exit at once)
-    hipLaunchKernelGGL(zd_k_execute, dim3(a.k4_grid && a.k4_grid < a.n_frames ? a.k4_grid : a.n_frames), dim3(64), 0,
-                       s, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
-                       (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, a.n_frames);
+  } else {
+    k3(0, a.n_seq);
+    if (fork)
+      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
+    if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
+    k4(0, a.n_frames, s);
+  }
   if (a.n_k4f && (a.kmask & 8))
     hipLaunchKernelGGL(zd_k_execute_lds, dim3(a.n_k4f), dim3(K4F_T), 0, s, a.src, a.out, frames, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,

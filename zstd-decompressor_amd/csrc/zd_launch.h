@@ -20,6 +20,8 @@ struct LaunchArgs {
   hipEvent_t fork = nullptr, join = nullptr;
   uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
   uint32_t k4_grid = 0;    // cap on K4 workgroups (persistent over frames); 0 = one per frame
+  bool overlap = false;    // K4 of frames [0, n_frames_a) on aux beside K3 of the rest
+  uint32_t n_frames_a = 0, n_seq_a = 0;   // list_seq[0, n_seq_a) = the blocks of those frames
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
