@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--corpus-cache", default=os.environ.get("ZD_CORPUS_CACHE"),
                     help="directory to keep the generated corpus in between runs (experiments)")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: also time gathering every rank's output to rank 0 (SURVEY §8e), reported apart")
     ap.add_argument("--experiment", action="store_true",
                     help="timing-only variants: do not stop on decode errors")
     args = ap.parse_args()
@@ -220,6 +222,23 @@ def main():
         del ref
         assert args.experiment or verified, "GPU output differs from the source bytes"
 
+    # ---- optional: gather of the decoded frames to rank 0 (never part of value) ----
+    gather = None
+    if dist and args.gather:
+        from zstd_decompressor import shard
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.time()
+        got = shard.gather_to_root(d_dst, info.out_bytes, rank, world)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tg = torch.tensor([time.time() - tg], dtype=torch.float64, device=dev)
+        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        gb = float(info.out_bytes) * world
+        gather = {"gather_ms": round(tg.item() * 1e3, 3),
+                  "decode_plus_gather_MBps": round(gb / (ms_per_step / 1e3 + tg.item()) / 1e6, 1)}
+        del got
+
     out_bytes = info.out_bytes
     comp_bytes = len(data)
     total_out = torch.tensor([float(out_bytes)], dtype=torch.float64, device=dev)
@@ -278,6 +297,8 @@ def main():
             "cpu_baseline": cpu,
             "verified_bit_exact": verified,
         }
+        if gather:
+            res["gather_to_rank0"] = gather
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()
