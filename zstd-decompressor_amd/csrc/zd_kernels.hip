@@ -745,10 +745,17 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
     count += K2_GROUP;
   }
   }
+  // symbol by symbol with the reference's checks; one window serves while
+  // its top p bits stay inside it (the tail from the fast loop: < 88 bits)
   int st = 0;
+  WinU w = winu_load(bs, base, pos);
+  int32_t p0 = pos;
   while (pos > 0 && !st) {
-    const WinU w = winu_load(bs, base, pos);
-    uint32_t idx = (uint32_t)(winu_top(w, 0) >> sh);
+    if ((p0 - pos) + (int32_t)w.sh > 100) {
+      w = winu_load(bs, base, pos);
+      p0 = pos;
+    }
+    uint32_t idx = (uint32_t)(winu_top(w, (uint32_t)(p0 - pos)) >> sh);
     if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
     const uint32_t e = lut[idx];
     const int32_t nb = (int32_t)((e >> 8) & 0x7F);
