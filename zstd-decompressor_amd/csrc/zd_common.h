@@ -80,7 +80,7 @@ ZD_HD inline uint32_t k3_entry(uint32_t e, int k) {
   else { eb = c; bad = c > 31; }
   return ns | ((eb & 31) << 10) | (bad ? K3_BAD : 0u);
 }
-// K3's fast chain (zd_kernels.hip seq_chainf) reads one number per table per
+// K3's fast chain (zd_kernels.hip seq_chainfl) reads one number per table per
 // step: nextState | (extra-bit count + state-bit count) << 10, with the
 // count 63 (never reached: <= 31 + 9) marking a code above the maximum.
 constexpr uint32_t K3F_BAD = 63u << 10;

@@ -541,43 +541,15 @@ __device__ inline uint64_t winu_top(const WinU& w, uint32_t d) {
   return k < 64 ? f : (w.w0 << (k & 63));
 }
 
-// 128-bit window of a backward bitstream: bits [wb, wb + 128) of the stream
-// (bit 0 = LSB of byte 0), loaded unaligned as the 16 bytes ending at the
-// byte that holds bit pos - 1, clamped at the input base.
 typedef uint32_t u32x4ua __attribute__((ext_vector_type(4), aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4ua g_u32x4ua;
-struct Win4 {
-  uint32_t w0, w1, w2, w3;
-  int32_t wb;
-};
-// m = base - s (<= 0): the lowest byte offset the window may start at.
-__device__ inline Win4 win4_load(const uint8_t* s, int32_t m, int32_t pos) {
-  const int32_t tb = (pos + 7) >> 3;
-  const int32_t o = max(tb - 16, m);
-  const u32x4ua v = *(g_u32x4ua*)(s + o);
-  Win4 w;
-  w.w0 = v.x; w.w1 = v.y; w.w2 = v.z; w.w3 = v.w;
-  w.wb = o * 8;
-  return w;
-}
-// The S bits [p - S, p) of the stream, S <= 32, MSB-first value; requires
-// wb <= p - S and p <= wb + 128 (else garbage, never a memory access).
-__device__ inline uint32_t win4_bits(const Win4& w, int32_t p, uint32_t S) {
-  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
-  const uint32_t k = y >> 5;
-  uint32_t lo = k == 0 ? w.w0 : w.w1;
-  uint32_t hi = k == 0 ? w.w1 : w.w2;
-  lo = k >= 2 ? w.w2 : lo;
-  hi = k >= 2 ? w.w3 : hi;
-  lo = k >= 3 ? w.w3 : lo;
-  hi = k >= 3 ? 0u : hi;
-  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
-}
 
-// The same chain with the bitstream window loaded two steps ahead: a
-// 24-byte window ending at the byte of pos_{i+1} covers every bit steps
-// i+1 and i+2 read (each step reads at most 63 extra + 27 state bits), so a
-// window load has a whole step more to land.
+// A backward bitstream window of 24 bytes: bits [wb, wb + 192) of the stream
+// (bit 0 = LSB of byte 0), loaded unaligned as the 24 bytes ending at the
+// byte that holds bit pos - 1, clamped at m = base - s (<= 0), the lowest
+// byte offset a window may start at.  Loaded at pos_{i+1}, it covers every
+// bit K3's steps i+1 and i+2 read (each step reads at most 63 extra + 27
+// state bits), so a window load has a whole step more to land.
 struct Win6 {
   uint32_t w0, w1, w2, w3, w4, w5;
   int32_t wb;
@@ -894,28 +866,18 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
 #define ZD_K3_LANES 16
 #endif
 constexpr int K3_LANES = ZD_K3_LANES;
-#ifdef ZD_K3_W1
-#define K3_CHAIN seq_chain       // window one step ahead (reference variant for experiments)
-#elif defined(ZD_K3_W3)
-#define K3_CHAIN seq_chain3      // window three steps ahead
-#else
-#define K3_CHAIN seq_chain2      // window two steps ahead (default: 23.8 -> 18.3 ms on C4)
-#endif
+#define K3_CHAIN seq_chain2      // the exact chain (windows two steps ahead)
 #ifndef ZD_K3_LA
 #define ZD_K3_LA 4                   // windows L steps ahead (C4: L2 17.3 ms, L3 14.5, L4 13.8)
 #endif
 #ifndef ZD_K3_WN
 #define ZD_K3_WN 6                   // window dwords
 #endif
-#if ZD_K3_LA == 2
-#define K3_FAST seq_chainf
-#else
 #define K3_FAST seq_chainfl<ZD_K3_LA, ZD_K3_WN>
-#endif
 #ifdef ZD_K3_EXACT
 #define K3_ENTRY(e, k, al) k3_entry(e, k)       // experiment: checks inside the chain (seq_chain2 on LDS)
 #else
-#define K3_ENTRY(e, k, al) k3f_entry(e, k, al)  // default: seq_chainf, exact chain from HBM on a reject
+#define K3_ENTRY(e, k, al) k3f_entry(e, k, al)  // default: seq_chainfl, exact chain from HBM on a reject
 #endif
 constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
@@ -928,74 +890,6 @@ __device__ inline void k3_store(uint64_t* p, uint32_t pos, uint32_t states) {
 #else
   *p = v;
 #endif
-}
-
-// One block's FSE chain.  TP: LDS (k3 entries) or HBM (sym entries, K3_SYM).
-// Returns 0 or the reference's error (the block then never executes).
-template <typename TP, bool K3_SYM>
-__device__ int seq_chain(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
-                         int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
-  // BackwardBitParser::new (parsing.rs:200-220)
-  if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
-  const uint8_t lastb = bs[bs_size - 1];
-  if (lastb == 0) return ZD_E_NULL_BYTE;
-  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
-  // SequenceDecoder::initialize: LL, OF, ML, each take(al) from the top (sequence.rs:59-65)
-  const int32_t A = all + alo + alm;
-  if (A > pos) return ZD_E_NOT_ENOUGH_BITS;
-  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-16);
-  Win4 w = win4_load(bs, m, pos);
-  const uint32_t v0 = win4_bits(w, pos, (uint32_t)A);
-  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
-  pos -= A;
-  w = win4_load(bs, m, pos);
-  // nb = AL - highbit(ns) = clz(ns) + (AL - 31); baseline = (ns << nb) - T
-  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
-  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
-  // Record i is stored at the end of step i - 1, after the load of step i's
-  // window: vmcnt drains in issue order, so each step waits for its window
-  // and never for the record store just before it.  The block's records
-  // have one spare slot past the last (host: seq_out), so the final step
-  // stores without a branch.
-  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
-  int st = 0;
-  for (uint32_t i = 0;; i++) {
-    uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
-    if (K3_SYM) {
-      eLL = k3_entry(eLL, 0);
-      eOF = k3_entry(eOF, 1);
-      eML = k3_entry(eML, 2);
-    }
-    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
-    // ns >= 1 in every table K1 builds: clz without the zero case
-    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
-    // update_symbol_value (sequence.rs:41-55) reads OF, ML, LL extra bits
-    const uint32_t E = ((eLL >> 10) & 31) + ((eML >> 10) & 31) + ((eOF >> 10) & 31);
-    const bool codemax = ((eLL | eML | eOF) & K3_BAD) != 0;
-    const bool last = i + 1 == n;
-    const uint32_t S = last ? 0 : nbL + nbM + nbO;
-    st = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : ((int32_t)(E + S) > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
-    // update_bits: LL, ML, OF (sequence.rs:80-88), below the extra bits
-    const int32_t p2 = pos - (int32_t)E;
-    const uint32_t v = win4_bits(w, p2, S);
-    pos = p2 - (int32_t)S;
-#if defined(ZD_EXP_NOLOAD)
-    w.wb = pos - 100;                                 // experiment: stale window bits, no load
-#else
-    w = win4_load(bs, m, pos);
-#endif
-    const uint32_t vO = __builtin_amdgcn_ubfe(v, 0, nbO), vM = __builtin_amdgcn_ubfe(v, nbO, nbM);
-    const uint32_t vL = v >> (nbO + nbM);
-    sLL = (nsL << nbL) + vL - TL;
-    sML = (nsM << nbM) + vM - TM;
-    sOF = (nsO << nbO) + vO - TO;
-    asm volatile("" ::: "memory");                    // the store stays below the load
-#ifndef ZD_EXP_NOSTORE
-    k3_store(out + i + 1, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
-#endif
-    if (st != 0 || last) break;
-  }
-  return st;
 }
 
 template <typename TP, bool K3_SYM>
@@ -1068,196 +962,6 @@ __device__ int seq_chain2(const uint8_t* bs, uint32_t bs_size, uintptr_t base, T
   return st;
 }
 
-// The chain with the window loaded three steps ahead: a 40-byte window
-// ending at the byte of pos_{i+1} covers every bit steps i+1..i+3 read
-// (3 x 90 bits + 7), at the price of a 10-way dword select per step.
-struct Win10 {
-  uint32_t w[10];
-  int32_t wb;
-};
-__device__ inline Win10 win10_load(const uint8_t* s, int32_t m, int32_t pos) {
-  const int32_t tb = (pos + 7) >> 3;
-  const int32_t o = max(tb - 40, m);
-  const u32x4ua v0 = *(g_u32x4ua*)(s + o);
-  const u32x4ua v1 = *(g_u32x4ua*)(s + o + 16);
-  const u32x2ua v2 = *(g_u32x2ua*)(s + o + 32);
-  Win10 w;
-  w.w[0] = v0.x; w.w[1] = v0.y; w.w[2] = v0.z; w.w[3] = v0.w;
-  w.w[4] = v1.x; w.w[5] = v1.y; w.w[6] = v1.z; w.w[7] = v1.w;
-  w.w[8] = v2.x; w.w[9] = v2.y;
-  w.wb = o * 8;
-  return w;
-}
-__device__ inline uint32_t win10_bits(const Win10& w, int32_t p, uint32_t S) {
-  const uint32_t y = (uint32_t)(p - (int32_t)S - w.wb);
-  const uint32_t k = y >> 5;
-  uint32_t lo = w.w[0], hi = w.w[1];
-#pragma unroll
-  for (int i = 1; i < 10; i++) {
-    lo = k >= (uint32_t)i ? w.w[i] : lo;
-    hi = k >= (uint32_t)i ? (i + 1 < 10 ? w.w[i + 1] : 0u) : hi;
-  }
-  return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
-}
-
-template <typename TP, bool K3_SYM>
-__device__ int seq_chain3(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tll, TP tml, TP tof, int all,
-                          int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
-  if (bs_size == 0) return ZD_E_EMPTY_INPUT_DATA;
-  const uint8_t lastb = bs[bs_size - 1];
-  if (lastb == 0) return ZD_E_NULL_BYTE;
-  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
-  const int32_t A = all + alo + alm;
-  if (A > pos) return ZD_E_NOT_ENOUGH_BITS;
-  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-40);
-  const int32_t pos0 = pos;
-  const Win10 wi = win10_load(bs, m, pos);
-  const uint32_t v0 = win10_bits(wi, pos, (uint32_t)A);
-  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
-  pos -= A;
-  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
-  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
-  // loop entry mirrors the loop's memory-op order (window, store) x 3
-  Win10 wa = win10_load(bs, m, pos0);            // step 0
-  asm volatile("" ::: "memory");
-  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
-  Win10 wb = win10_load(bs, m, pos);             // step 1
-  asm volatile("" ::: "memory");
-  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
-  Win10 wc = win10_load(bs, m, pos);             // step 2 (pos_2 >= pos_0 - 180)
-  asm volatile("" ::: "memory");
-  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
-  int st = 0;
-  uint32_t i = 0;
-  auto step = [&](Win10& use, bool live) -> bool {
-    uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
-    if (K3_SYM) {
-      eLL = k3_entry(eLL, 0);
-      eOF = k3_entry(eOF, 1);
-      eML = k3_entry(eML, 2);
-    }
-    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
-    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
-    const uint32_t E = ((eLL >> 10) & 31) + ((eML >> 10) & 31) + ((eOF >> 10) & 31);
-    const bool codemax = ((eLL | eML | eOF) & K3_BAD) != 0;
-    const bool last = i + 1 >= n;
-    const uint32_t S = last ? 0 : nbL + nbM + nbO;
-    const int sst = codemax ? ZD_E_SEQUENCE_CODE_MAX_EXCEEDED : ((int32_t)(E + S) > pos ? ZD_E_NOT_ENOUGH_BITS : 0);
-    st = live ? sst : st;
-    const int32_t p2 = pos - (int32_t)E;
-    const uint32_t v = win10_bits(use, p2, S);
-    pos = p2 - (int32_t)S;
-    use = win10_load(bs, m, pos);                  // for step i + 3
-    const uint32_t vO = __builtin_amdgcn_ubfe(v, 0, nbO), vM = __builtin_amdgcn_ubfe(v, nbO, nbM);
-    const uint32_t vL = v >> (nbO + nbM);
-    sLL = (nsL << nbL) + vL - TL;
-    sML = (nsM << nbM) + vM - TM;
-    sOF = (nsO << nbO) + vO - TO;
-    asm volatile("" ::: "memory");
-    k3_store(out + (live ? i + 1 : n), (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
-    i++;
-    return !live || sst != 0 || last;
-  };
-  for (;;) {
-    const bool d1 = step(wa, true);
-    const bool d2 = step(wb, !d1);
-    const bool d3 = step(wc, !d2);
-    if (d3) break;
-  }
-  return st;
-}
-
-// 32 bits of a 24-byte window from bit y up (y <= 192; bits past the window read as zero).
-__device__ inline uint32_t win6_at(const Win6& w, uint32_t y) {
-  const uint32_t k = y >> 5;
-  uint32_t lo = k == 0 ? w.w0 : w.w1;
-  uint32_t hi = k == 0 ? w.w1 : w.w2;
-  lo = k >= 2 ? w.w2 : lo;
-  hi = k >= 2 ? w.w3 : hi;
-  lo = k >= 3 ? w.w3 : lo;
-  hi = k >= 3 ? w.w4 : hi;
-  lo = k >= 4 ? w.w4 : lo;
-  hi = k >= 4 ? w.w5 : hi;
-  lo = k >= 5 ? w.w5 : lo;
-  hi = k >= 5 ? 0u : hi;
-  return __builtin_amdgcn_alignbit(hi, lo, y & 31);
-}
-
-// The fast chain: no checks inside the loop.  Each table gives nextState and
-// the step's total bit count for that table (k3f_entry), so a step is
-// pos -= tLL + tML + tOF, then the LL | ML | OF state bits are the low bits
-// at the new position.  Steps 0 .. n-2 update the states (a lane whose count
-// is odd runs step n-1 too, storing into the spare slot); the epilogue
-// re-reads record n-1 and checks the last step (extra bits only,
-// sequences.rs:223-229).  Anything the reference would reject -- a code
-// above the maximum anywhere (K3F_BAD), the position going negative before
-// the last step, or the last step's extra bits running out -- and the block
-// is decoded again by the exact chain, which finds the reference's error.
-// Returns 1 when the block needs the exact chain, else 0.
-__device__ int seq_chainf(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tll,
-                          const lds_u16* tml, const lds_u16* tof, int all, int alo, int alm, uint32_t n,
-                          uint64_t* __restrict__ out) {
-  if (bs_size == 0) return 1;
-  const uint8_t lastb = bs[bs_size - 1];
-  if (lastb == 0) return 1;
-  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
-  const int32_t A = all + alo + alm;
-  if (A > pos) return 1;
-  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-24);
-  const int32_t pos0 = pos;
-  const Win6 wi = win6_load(bs, m, pos);
-  const uint32_t v0 = win6_bits(wi, pos, (uint32_t)A);
-  uint32_t sLL = v0 >> (alo + alm), sOF = __builtin_amdgcn_ubfe(v0, alm, alo), sML = __builtin_amdgcn_ubfe(v0, 0, alm);
-  pos -= A;
-  const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
-  const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
-  // Two records per 16-byte store, after both steps' window loads; the loop
-  // entry repeats that order (window, window, store).
-  typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(8)));
-  const uint64_t r0 = (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
-  Win6 wa = win6_load(bs, m, pos0);
-  Win6 wb = win6_load(bs, m, pos);
-  asm volatile("" ::: "memory");
-  *(u64x2u*)out = u64x2u{r0, r0};                 // slot 1: rewritten by the loop, or the spare
-  uint32_t mx = 0;
-  auto step = [&](Win6& use) -> uint64_t {
-    const uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
-    mx = max(mx, max(eLL, max(eML, eOF)));
-    const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
-    const uint32_t nbL = __builtin_clz(nsL) + aL, nbM = __builtin_clz(nsM) + aM, nbO = __builtin_clz(nsO) + aO;
-    pos -= (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10));
-    const uint32_t r = win6_at(use, (uint32_t)(pos - use.wb));
-#if defined(ZD_EXP_NOLOAD)
-    use.wb = pos - 100;                            // experiment: stale window bits, no load
-#else
-    use = win6_load(bs, m, pos);                   // for the step after next
-#endif
-    const uint32_t vO = __builtin_amdgcn_ubfe(r, 0, nbO), vM = __builtin_amdgcn_ubfe(r, nbO, nbM);
-    const uint32_t vL = __builtin_amdgcn_ubfe(r, nbO + nbM, nbL);
-    sLL = (nsL << nbL) + vL - TL;
-    sML = (nsM << nbM) + vM - TM;
-    sOF = (nsO << nbO) + vO - TO;
-    return (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
-  };
-  for (uint32_t i = 0; i + 1 < n; i += 2) {
-    const uint64_t ra = step(wa);
-    const uint64_t rb = step(wb);                  // slot n when n - 1 is odd: the spare
-    asm volatile("" ::: "memory");
-#ifndef ZD_EXP_NOSTORE
-    *(u64x2u*)(out + i + 1) = u64x2u{ra, rb};
-#endif
-  }
-  // the last step: its extra bits only
-  const uint64_t rl = *(volatile uint64_t*)(out + n - 1);
-  const int32_t pl = (int32_t)(uint32_t)rl;
-  const uint32_t st = (uint32_t)(rl >> 32);
-  const uint32_t eLL = tll[st & 1023], eML = tml[(st >> 10) & 1023], eOF = tof[(st >> 20) & 1023];
-  mx = max(mx, max(eLL, max(eML, eOF)));
-  const uint32_t S = (__builtin_clz(eLL & 1023) + aL) + (__builtin_clz(eML & 1023) + aM) + (__builtin_clz(eOF & 1023) + aO);
-  const int32_t E = (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10) - S);
-  return (mx >= K3F_BAD || pl < 0 || E > pl) ? 1 : 0;
-}
-
 // N-dword bitstream window ending at the byte of pos (clamped to start at m).
 template <int N>
 struct WinN {
@@ -1294,12 +998,22 @@ __device__ inline uint32_t winn_at(const WinN<N>& w, uint32_t y) {
   return __builtin_amdgcn_alignbit(hi, lo, y & 31);
 }
 
-// seq_chainf with windows loaded L steps ahead (a ring of L windows).  A
-// 24-byte window ending at the byte of pos_{i+1} covers steps i+1..i+L when
-// they read <= 185 bits together (text: ~35 bits a step); a lane whose steps
-// read more sees a window start above its position (ymin < 0) and the block
-// goes to the exact chain.  U steps per trip, records stored in pairs; a pair
-// past the block's last record goes to its two spare slots (host: seq_out).
+// The fast chain: no checks inside the loop.  Each table gives nextState and
+// the step's total bit count for that table (k3f_entry), so a step is
+// pos -= tLL + tML + tOF, then the LL | ML | OF state bits are the low bits
+// at the new position.  Steps 0 .. n-2 update the states (a lane whose count
+// runs past n-1 stores into the spare slots); the epilogue re-reads record
+// n-1 and checks the last step (extra bits only, sequences.rs:223-229).
+// Windows are loaded L steps ahead (a ring of L): a 4N-byte window ending at
+// the byte of pos_{i+1} covers steps i+1..i+L when they read <= 32 N - 7
+// bits together (text: ~35 bits a step).  Anything the reference would
+// reject -- a code above the maximum anywhere (K3F_BAD), the position going
+// negative before the last step, the last step's extra bits running out --
+// or a window that did not cover its step (ymin < 0), and the block is
+// decoded again by the exact chain, which finds the reference's error.  U
+// steps per trip, records stored in pairs; a pair past the block's last
+// record goes to its two spare slots (host: seq_out).  Returns 1 when the
+// block needs the exact chain, else 0.
 template <int L, int N>
 __device__ int seq_chainfl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tll,
                            const lds_u16* tml, const lds_u16* tof, int all, int alo, int alm, uint32_t n,
