@@ -239,3 +239,39 @@ def test_k1_large_tables():
             hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
             frame = b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x00]) + hdr + content
             assert_parity(frame, False, f"nsym {nsym} al {al} trial {trial}", allow_ood=True)
+
+
+def _deep_tree_frame(r, nbytes):
+    """One frame, one compressed block: a Huffman tree of maxBits 12 (direct
+    weights 12, 11, ..., 1 and the implied last symbol) over a random literal
+    bitstream (every bit pattern decodes: the tree is complete), then one
+    sequence from random bits with the predefined tables."""
+    weights = list(range(12, 0, -1))                       # symbols 0..11; symbol 12 implied
+    desc = bytes([127 + len(weights)]) + bytes((weights[i] << 4) | weights[i + 1] for i in range(0, 12, 2))
+    stream = bytes(r.randrange(256) for _ in range(nbytes - 1)) + bytes([r.randrange(1, 256)])
+    comp = len(desc) + len(stream)
+    regen = 1023                                            # >= what the stream decodes (the reference ignores it, D8)
+    lh = (2 | (0 << 2) | (regen << 4) | (comp << 14)).to_bytes(3, "little")   # compressed, 1 stream
+    seqs = bytes([1, 0x00]) + bytes(r.randrange(256) for _ in range(4)) + bytes([r.randrange(1, 256)])
+    content = lh + desc + stream + seqs                     # one sequence, predefined tables
+    hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
+    return b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x50]) + hdr + content
+
+
+def test_k2_deep_trees_beside_libzstd_frames():
+    """12-bit Huffman trees (K2 reads their LUTs from HBM, and so does every
+    block of its workgroup) in between libzstd frames with <= 11-bit trees,
+    whose LUTs hold K2's shifted width field (zd_kernels.hip lut_field)."""
+    r = random.Random(9)
+    deep_ok, deep_err = [], []
+    while len(deep_ok) < 8 or len(deep_err) < 8:         # frames the reference decodes, and ones it rejects
+        f = _deep_tree_frame(r, r.randrange(20, 200))
+        (deep_err if oracle.decompress_status(f, False)[0] else deep_ok).append(f)
+    src = gen.text(300_000, seed=4)
+    parts = []
+    for i in range(24):
+        parts.append(deep_ok[i // 3] if i % 3 == 1 else gen.frames(src[i * 12_000:(i + 1) * 12_000], 12_000, 3))
+    ost, _ = assert_parity(b"".join(parts), False, "deep trees + libzstd frames")
+    assert ost == 0
+    for i, f in enumerate(deep_err[:8]):
+        assert_parity(f, False, f"deep tree, rejected #{i}")

@@ -256,6 +256,17 @@ struct K1LaneS {
   uint16_t cnt[16], start[16], placed[16];
 };
 
+// A LUT entry's bits 8-14: the code width (or an absent node's depth) f.
+// Trees K2 decodes from LDS (p <= K2 LUT bits, 11) store (32 - f) & 31
+// instead: K2's fast loop shifts its 64-bit bit window as two 32-bit halves,
+// hi = alignbit(hi, lo, 32 - f), one 32-bit op on the symbol chain.
+constexpr int K2_LUT_BITS = 11;
+__device__ inline uint32_t lut_field(uint32_t f, int p) { return p <= K2_LUT_BITS ? (32 - f) & 31 : f; }
+__device__ inline uint32_t lut_width(uint32_t e, bool s32) {
+  const uint32_t f = (e >> 8) & 0x7F;
+  return s32 ? (32 - f) & 31 : f;
+}
+
 // Entries [a, b) that no code reaches: the tree node there is Absent.  Its
 // depth is that of the largest aligned block around the entry inside [a, b)
 // (the entries just outside hold codes or lie past the table), which is the
@@ -268,7 +279,7 @@ __device__ void lut_holes(uint16_t* lut, int p, uint32_t a, uint32_t b) {
       const uint32_t lo = e & ~((1u << k) - 1);
       if (lo >= a && lo + (1u << k) <= b) break;
     }
-    lut[e] = (uint16_t)(LUT_ABSENT | ((uint32_t)(p - k) << 8));
+    lut[e] = (uint16_t)(LUT_ABSENT | (lut_field((uint32_t)(p - k), p) << 8));
   }
 }
 
@@ -387,7 +398,7 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
     if (r >= L.placed[w]) continue;
     const uint32_t S = 1u << (p - w);
     const uint32_t at = L.start[w] + r * S;
-    const uint16_t ent = (uint16_t)((i & 0xFF) | ((uint32_t)w << 8));
+    const uint16_t ent = (uint16_t)((i & 0xFF) | (lut_field((uint32_t)w, p) << 8));
     if (S >= 4) {
       const uint64_t e4 = (uint64_t)ent * 0x0001000100010001ull;
       for (uint32_t e = 0; e < S; e += 4) *(uint64_t*)(lut + at + e) = e4;
@@ -582,11 +593,6 @@ __device__ inline uint32_t win6_bits(const Win6& w, int32_t p, uint32_t S) {
   return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hi, lo, y & 31), 0, S);
 }
 
-#ifdef ZD_K2_W1
-constexpr bool K2_WIN2 = false;   // experiment: K2 windows one group ahead only
-#else
-constexpr bool K2_WIN2 = true;
-#endif
 
 // The 64 bits below q of a 24-byte window, MSB-first (q - 32 >= wb, q <= wb + 192;
 // bits below the window read as zero: K2 looks at the top 44 only).
@@ -619,7 +625,6 @@ __device__ inline uint64_t win6_top64(const Win6& w, int32_t q) {
 #endif
 constexpr int K2_BLOCKS = ZD_K2_BLOCKS;
 constexpr int K2_LANES = 4 * K2_BLOCKS;
-constexpr int K2_LUT_BITS = 11;
 constexpr int K2_GROUP = 8;
 static_assert(K2_LANES <= 64, "K2 workgroup must be a single wave");
 static_assert(K2_GROUP * LUT_MAX_BITS <= 97, "a group must fit one window");
@@ -642,7 +647,7 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
   const uint32_t sh = 64 - p;
-  if constexpr (K2_WIN2 && std::is_same<LP, const lds_u16*>::value) {
+  if constexpr (std::is_same<LP, const lds_u16*>::value) {
     // LDS LUT (maxBits <= 11, a group reads <= 88 bits): 24-byte windows
     // two groups ahead.  The window loaded when group g ends (ending at the
     // byte of pos_{g+1}) covers groups g+1 and g+2, so group g+2 reads it and
@@ -662,16 +667,19 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
       uint32_t used = 0, bad = 0;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        uint64_t t = win6_top64(w, pos - (int32_t)used);
+        const uint64_t t = win6_top64(w, pos - (int32_t)used);
+        uint32_t hi = (uint32_t)(t >> 32), lo = (uint32_t)t, ssum = 0;
 #pragma unroll
         for (int j = 0; j < K2_GROUP / 2; j++) {
-          const uint32_t e = lut[(uint32_t)(t >> sh)];
-          const uint32_t nb = (e >> 8) & 0x7F;
+          const uint32_t e = lut[hi >> (sh - 32)];
+          const uint32_t sf = e >> 8;                 // 32 - width (and the absent flag, bit 7)
           bad |= e & LUT_ABSENT;
-          t <<= nb;
-          used += nb;
+          hi = __builtin_amdgcn_alignbit(hi, lo, sf);
+          lo = __builtin_amdgcn_alignbit(lo, 0u, sf);
+          ssum += sf & 31;
           acc |= (uint64_t)(e & 0xFF) << (8 * (h * (K2_GROUP / 2) + j));
         }
+        used += 32 * (K2_GROUP / 2) - ssum;
       }
       const bool ok = live && !bad;
       pos = ok ? pos - (int32_t)used : pos;
@@ -702,7 +710,7 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
 #pragma unroll
       for (int j = 0; j < K2_GROUP / 2; j++) {
         const uint32_t e = lut[(uint32_t)(t >> sh)];
-        const uint32_t nb = (e >> 8) & 0x7F;
+        const uint32_t nb = lut_width(e, p <= K2_LUT_BITS);
         bad |= e & LUT_ABSENT;
         t <<= nb;
         used += nb;
@@ -730,7 +738,7 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
     uint32_t idx = (uint32_t)(winu_top(w, (uint32_t)(p0 - pos)) >> sh);
     if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
     const uint32_t e = lut[idx];
-    const int32_t nb = (int32_t)((e >> 8) & 0x7F);
+    const int32_t nb = (int32_t)lut_width(e, p <= K2_LUT_BITS);
     if (e & LUT_ABSENT) st = nb <= pos ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
     else if (nb > pos) st = ZD_E_NOT_ENOUGH_BITS;
     else {
