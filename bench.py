@@ -64,13 +64,14 @@ def cpu_baseline(frame_set: bytes, threads: int, budget_s: float = 20.0):
         out0 += len(oracle.frame_decode(frame_set[o:o + s])[1])
     per_byte = (time.time() - t0) / max(out0, 1)
     want = int(budget_s * threads / max(per_byte, 1e-12))
-    total_out = sum(1 for _ in ())
+    sizes = [f["content_size"] if f["content_size"] is not None and f["content_size"] >= 0 else 128 << 10
+             for f in frames]
     sample, acc = [], 0
     i = 0
     while acc < want and i < len(spans) * 4:
         o, s = spans[i % len(spans)]
         sample.append((o, s))
-        acc += 128 << 10
+        acc += sizes[i % len(spans)]
         i += 1
 
     def work(chunk):
@@ -84,9 +85,40 @@ def cpu_baseline(frame_set: bytes, threads: int, budget_s: float = 20.0):
     with cf.ThreadPoolExecutor(threads) as ex:
         total_out = sum(ex.map(work, parts))
     dt = time.time() - t0
-    return {"value": round(total_out / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
-            "sample": f"{len(sample)} frames ({total_out / 2**20:.0f} MiB decoded) of the same corpus, "
-                      f"oracle/zd_oracle.c on {threads} host threads, {dt:.1f} s"}
+    res = {"value": round(total_out / dt / 1e6, 2), "unit": "MB/s", "cores": threads, "kind": "port",
+           "sample": f"{len(sample)} frames ({total_out / 2**20:.0f} MiB decoded) of the same corpus, "
+                     f"oracle/zd_oracle.c on {threads} host threads, {dt:.1f} s"}
+    return res, (sample, [sizes[k % len(spans)] for k in range(len(sample))])
+
+
+def cpu_libzstd(frame_set: bytes, sample, threads: int):
+    """Context only (not the contract's cpu_baseline): the system libzstd,
+    an optimised RFC decoder (SURVEY.md §8d ii), on the same frame sample."""
+    import ctypes as C
+    from corpus import libzstd
+    L = libzstd.lib()
+    spans, sizes = sample
+    buf = C.create_string_buffer(frame_set, len(frame_set))
+    base = C.addressof(buf)
+
+    def work(idx):
+        n = 0
+        for k in idx:
+            (o, s), cap = spans[k], sizes[k]
+            out = C.create_string_buffer(cap)
+            r = L.ZSTD_decompress(out, cap, base + o, s)
+            if L.ZSTD_isError(r):
+                raise RuntimeError(L.ZSTD_getErrorName(r))
+            n += r
+        return n
+    parts = [list(range(k, len(spans), threads)) for k in range(threads)]
+    t0 = time.time()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(work, parts))
+    dt = time.time() - t0
+    return {"value": round(total / dt / 1e6, 2), "unit": "MB/s", "cores": threads,
+            "sample": f"the cpu_baseline sample ({total / 2**20:.0f} MiB), libzstd "
+                      f"{L.ZSTD_versionNumber()} ZSTD_decompress on {threads} host threads, {dt:.2f} s"}
 
 
 def traffic_of(kernel: str, args):
@@ -251,10 +283,14 @@ def main():
     dom_ms = kt[dom]
     achieved = alg_per_launch / (dom_ms / 1e3) / 1e9
 
-    cpu = None
+    cpu = cpu_zstd = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and src is not None:
         threads = min(args.cpu_threads, os.cpu_count() or 1)
-        cpu = cpu_baseline(frame_set, threads)
+        cpu, sample = cpu_baseline(frame_set, threads)
+        try:
+            cpu_zstd = cpu_libzstd(frame_set, sample, threads)
+        except Exception as ex:                     # context only: never fails the bench
+            cpu_zstd = {"error": str(ex)[:200]}
 
     if rank == 0:
         res = {
@@ -295,6 +331,7 @@ def main():
             },
             "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
             "cpu_baseline": cpu,
+            "cpu_libzstd": cpu_zstd,
             "verified_bit_exact": verified,
         }
         if gather:
