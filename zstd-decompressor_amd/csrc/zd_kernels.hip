@@ -141,6 +141,10 @@ struct FwBits {
 // A table needs K1's large scratch (more than K1S_SYMS symbols, or a
 // Huffman-weight table deeper than AL 6): the block goes to the second pass.
 constexpr int K1_BIG = 1;
+// A Huffman-weight stream past 253 weights: the reference keeps decoding (and
+// may never stop: every remaining state can read 0 bits, huffman.rs:121-124),
+// which the GPU path does not follow -- out of domain at the tree's parse.
+constexpr int K1_OOD_PARSE = 2;
 constexpr uint32_t K1S_SYMS = 64;
 
 // parse_fse_table (fse.rs:16-69); dist holds max_sym entries (256: all)
@@ -316,7 +320,7 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
         uint32_t w;
         if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
         else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
-        if (nw >= K1_MAX_WEIGHTS - 2) { st = ZD_E_OUT_OF_DOMAIN; break; }
+        if (nw >= K1_MAX_WEIGHTS - 2) { st = K1_OOD_PARSE; break; }
         L.weights[nw++] = (uint8_t)w;
         uint32_t& sx = last_updated_is_first ? sb : sa;
         bool& has = last_updated_is_first ? has_b : has_a;
@@ -475,6 +479,10 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
     const int st = k1_huffman_lane(blk + C.lit_data, src, src + src_size, L, luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
     if (!BIG && st == K1_BIG) {
       cstate[ci].k1_big = 1;
+      return;
+    }
+    if (st == K1_OOD_PARSE) {
+      key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_HUF_DESC, 0, ZD_E_OUT_OF_DOMAIN));
       return;
     }
     if (st == ZD_E_OUT_OF_DOMAIN) {
