@@ -519,6 +519,9 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   return 0;
 }
 
+constexpr size_t FORK_MAX_SEQ_BLOCKS = 256 * 16;   // MI355X CUs x K3 chains per workgroup
+constexpr size_t FORK_MIN_SEQ_BLOCKS = 256;
+
 int upload_plan(zd_plan* P) {
   HIPCHK(hipMalloc(&P->d_ws, P->W.total));
   auto up = [&](uint64_t off, const void* p, size_t bytes) -> int {
@@ -708,9 +711,15 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
-  // K2 beside K3 on a second stream measured slower on C4 (61.4 vs 57.9 ms:
-  // K3 is LDS-bound and K2 takes its CUs), so it is opt-in (ZD_FORK=1)
-  static const bool fork = getenv("ZD_FORK") && atoi(getenv("ZD_FORK")) == 1;
+  // K2 beside K3 on a second stream: measured slower on C4 (61.4 vs 57.9 ms:
+  // K3 is LDS-bound and K2 takes its CUs), so it is taken only when K3's
+  // chains use at most one workgroup per CU (<= 256 x 16 blocks: the few-
+  // frames regime, where both kernels run one round at their chain latency)
+  // and there are enough of them for the overlap to pay for a second stream;
+  // ZD_FORK=1 / 0 forces it on / off
+  static const char* fork_env = getenv("ZD_FORK");
+  const bool fork = fork_env ? atoi(fork_env) == 1
+                             : P->list_seq.size() >= FORK_MIN_SEQ_BLOCKS && P->list_seq.size() <= FORK_MAX_SEQ_BLOCKS;
   static const bool overlap = getenv("ZD_OVERLAP") && atoi(getenv("ZD_OVERLAP")) == 1;
   if (overlap && !fork && P->fdesc.size() > 1) {
     // K4 of the first half of the frames beside K3 of the second half
