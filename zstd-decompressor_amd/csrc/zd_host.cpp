@@ -340,6 +340,8 @@ namespace {
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 4096;
+
 // Builds device-side descriptors from the host frames.  `prev_*` seed the
 // Treeless/Repeat resolution (context API), -1 when absent.
 int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
@@ -349,6 +351,9 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   bool exact = true;
   P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
   P->frame_cap_off.clear();
+  static const char* k4f_env = getenv("ZD_K4F");
+  const bool k4f_on = k4f_env ? atoi(k4f_env) == 1
+                              : P->frames.size() >= K4F_AUTO_MIN_FRAMES && P->frames.size() <= K4F_AUTO_MAX_FRAMES;
   for (size_t fi = 0; fi < P->frames.size(); fi++) {
     HostFrame& hf = P->frames[fi];
     FrameDesc fd{};
@@ -452,10 +457,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
       fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
     fd.out = out_off;
     fd.out_cap = cap;
-    // K4F (whole frame resident in LDS) is an experimental executor, off by
-    // default (slower than the streaming K4 on C4); ZD_K4F=1 routes
-    // every frame that fits to it
-    static const bool k4f_on = getenv("ZD_K4F") && atoi(getenv("ZD_K4F")) == 1;
+    // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
+    // executes the frames that fit it in plans of 256-4096 frames, where the
+    // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
+    // it is slower on C4.  ZD_K4F=1 / 0 forces it on / off.
     fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
     if (fd.lds) P->list_k4f.push_back((uint32_t)fi);
     // Leading raw / RLE blocks (skippable payloads too) have output offsets
