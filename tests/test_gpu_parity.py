@@ -172,6 +172,30 @@ def test_corrupted_inputs():
     assert stats["ok"] + stats["err_same"] >= 290, stats
 
 
+def test_corrupted_inputs_forked_plan():
+    """Corruptions inside a 300-frame plan: plans of 256-4096 frames take the
+    few-frames path (K1's Huffman half + K2 on a second stream beside K1's
+    sequence half + K3, then K4F; zd_host.cpp FORK_* / K4F_AUTO_*), whose
+    error keys come from both streams.  Same first error and partial output
+    as the oracle."""
+    r = random.Random(77)
+    src = gen.text(300 * 4096, seed=12)
+    base = gen.frames(src, 4096, 3)
+    from zstd_decompressor.batch import frames_index
+    spans = [(f["src_offset"], f["src_size"]) for f in frames_index(base)[0]]
+    assert len(spans) == 300
+    assert_parity(base, False, "forked plan, intact")
+    stats = {"ok": 0, "err_same": 0, "ood": 0}
+    for it in range(60):
+        d = bytearray(base)
+        o, n = spans[r.randrange(20, 280)]
+        for _ in range(r.randrange(1, 4)):
+            d[o + r.randrange(n)] = r.randrange(256)
+        ost, gst = assert_parity(bytes(d), False, f"forked corrupt #{it}", allow_ood=True)
+        stats["ok" if ost == 0 else ("ood" if gst == OUT_OF_DOMAIN else "err_same")] += 1
+    assert stats["ok"] + stats["err_same"] >= 55, stats
+
+
 def test_many_frame_roundtrip_large():
     """Size-independent property at a larger size: decode(compress(x)) == x,
     and the per-frame statuses are all OK."""

@@ -286,7 +286,9 @@ struct CompState {
   uint32_t stop;           // nonzero: literals/sequences stage failed or is out of domain
   uint8_t al[3];           // accuracy log of the LL/OF/ML table in this block's FSE slot
   uint8_t huf_bits;        // maxBits of this block's LUT
-  uint32_t k1_big;         // K1: tables need the large scratch (second pass)
+  uint8_t k1_bigh;         // K1: the Huffman table needs the large scratch (second pass)
+  uint8_t k1_bigs;         // K1: a sequence table needs it
+  uint8_t pad[2];
 };
 
 // Blocks of frames in order (all types).

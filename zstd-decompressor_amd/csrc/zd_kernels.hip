@@ -457,9 +457,13 @@ __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, LN& L, 
 }
 
 // Two passes: every block with the small scratch (K1LaneS), then the blocks
-// that flagged k1_big with the large one (the same code; the first pass
-// records nothing for them).
-template <bool BIG>
+// that flagged k1_bigh / k1_bigs with the large one (the same code; the first
+// pass records nothing for them).  PART: 1 the Huffman table (for K2), 2 the
+// sequence tables (for K3), 3 both.  With the K2 | K3 fork the two parts run
+// on the two streams: each writes its own CompState bytes, and a Huffman
+// parse error still decides the frame's error (key_min: its stage sorts
+// before the sequence tables' within a block).
+template <bool BIG, int PART>
 __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restrict__ src, uint64_t src_size,
                                                         const CompBlock* __restrict__ comp, CompState* cstate,
                                                         FrameState* fstate, const uint32_t* __restrict__ list,
@@ -470,15 +474,15 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
   if (li >= n_list) return;
   LN& L = lanes[threadIdx.x];
   const uint32_t ci = list[li];
-  if (BIG && !cstate[ci].k1_big) return;
+  if (BIG && !(((PART & 1) && cstate[ci].k1_bigh) || ((PART & 2) && cstate[ci].k1_bigs))) return;
   const CompBlock C = comp[ci];
   if (C.prebuilt) return;
   const uint8_t* blk = src + C.src;
-  if (C.lit_type == LIT_COMPRESSED && C.host_stage > PS_HUF_DESC) {
+  if ((PART & 1) && C.lit_type == LIT_COMPRESSED && C.host_stage > PS_HUF_DESC) {
     int p = 0;
     const int st = k1_huffman_lane(blk + C.lit_data, src, src + src_size, L, luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
     if (!BIG && st == K1_BIG) {
-      cstate[ci].k1_big = 1;
+      cstate[ci].k1_bigh = 1;
       return;
     }
     if (st == K1_OOD_PARSE) {
@@ -498,13 +502,13 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
       cstate[ci].huf_bits = (uint8_t)p;
     }
   }
-  if (C.nseq > 0 && C.host_stage > PS_SEQ_TABLES) {
+  if ((PART & 2) && C.nseq > 0 && C.host_stage > PS_SEQ_TABLES) {
     uint8_t al[3] = {0, 0, 0};
     uint32_t bo = 0, bsz = 0;
     int sub = 0;
     const int st = k1_sequences_lane(blk, C, L, fses + (uint64_t)C.fse_slot * FSE_SLOT, al, &bo, &bsz, &sub);
     if (!BIG && st == K1_BIG) {
-      cstate[ci].k1_big = 1;
+      cstate[ci].k1_bigs = 1;
       return;
     }
     for (int k = 0; k < 3; k++)
@@ -2351,21 +2355,30 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_rawcopy, dim3(a.n_copies), dim3(256), 0, s, a.src, a.out,
                        (const CopyDesc*)(ws + W.copies));
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
-  if (a.n_tables && (a.kmask & 1)) {
-    hipLaunchKernelGGL(zd_k_tables<false>, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
-                       a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
-    hipLaunchKernelGGL(zd_k_tables<true>, dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s, a.src,
-                       a.src_size, comp, cstate, fstate, (const uint32_t*)(ws + W.list_tables), a.n_tables, luts, fses);
-  }
-  if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
-  // K2 and K3 are independent once K1 is done: K2 runs on the aux stream
-  // beside K3 (not when timing kernels one by one)
+  // K2 and K3 are independent once their tables exist: with the fork, K1's
+  // Huffman half and K2 run on the aux stream beside K1's sequence half and
+  // K3 (not when timing kernels one by one)
   const bool fork = a.aux && !a.overlap && !a.events && a.n_huf && a.n_seq && (a.kmask & 6) == 6;
   hipStream_t s2 = fork ? a.aux : s;
   if (fork) {
     if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
   }
+  auto k1 = [&](auto pass_small, auto pass_big, hipStream_t st) {
+    const dim3 g((a.n_tables + K1_LANES - 1) / K1_LANES), b(K1_LANES);
+    const uint32_t* lt = (const uint32_t*)(ws + W.list_tables);
+    hipLaunchKernelGGL(pass_small, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses);
+    hipLaunchKernelGGL(pass_big, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses);
+  };
+  if (a.n_tables && (a.kmask & 1)) {
+    if (fork) {
+      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2);
+      k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s);
+    } else {
+      k1(zd_k_tables<false, 3>, zd_k_tables<true, 3>, s);
+    }
+  }
+  if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   if (a.n_huf && (a.kmask & 2))
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s2, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
