@@ -356,6 +356,8 @@ def main():
             },
             "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
             "host_plan_ms": round(host_plan_s * 1e3, 1),
+            "host_plan_split_ms": {"headers_and_descriptors": round(info.host_ns / 1e6, 1),
+                                   "workspace_alloc_and_upload": round(info.device_ns / 1e6, 1)},
             "value_incl_host_plan": round(total_out.item() / (ms_per_step / 1e3 + host_plan_s) / 1e6, 1),
             "cpu_baseline": cpu,
             "cpu_libzstd": cpu_zstd,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 1
+#define ZD_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -150,6 +150,8 @@ typedef struct zd_plan_info {
   uint64_t nliterals;      /* sum of Regenerated_Size over compressed-literal blocks */
   int32_t  index_status;   /* status of the host walk (first failing frame) */
   uint32_t _pad;
+  uint64_t host_ns;        /* zd_plan_create: header walk + descriptors (host work) */
+  uint64_t device_ns;      /* zd_plan_create: workspace allocation + descriptor upload */
 } zd_plan_info;
 
 /* Index src[0..n) on the host and allocate the plan's device workspace.

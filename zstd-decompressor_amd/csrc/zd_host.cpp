@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -641,13 +642,18 @@ int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) 
   zd_plan* P = new (std::nothrow) zd_plan();
   if (!P) return ZD_E_NO_MEMORY;
   P->flags = flags;
+  const auto t0 = std::chrono::steady_clock::now();
   plan_index(P, src, n);
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {1, 4, 8};
   build_plan(P, -1, none, 0, rep0, 0);
   P->info.src_bytes = n;
+  const auto t1 = std::chrono::steady_clock::now();
   int r = upload_plan(P);
   if (r) { zd_plan_destroy(P); return r; }
+  const auto t2 = std::chrono::steady_clock::now();
+  P->info.host_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+  P->info.device_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
   *out = P;
   return ZD_OK;
 }

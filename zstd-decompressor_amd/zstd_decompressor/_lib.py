@@ -42,7 +42,8 @@ class PlanInfo(C.Structure):
     _fields_ = [("nframes", C.c_uint64), ("nblocks", C.c_uint64), ("ncompressed", C.c_uint64),
                 ("src_bytes", C.c_uint64), ("out_bytes", C.c_uint64), ("out_exact", C.c_uint64),
                 ("workspace_bytes", C.c_uint64), ("nsequences", C.c_uint64), ("nliterals", C.c_uint64),
-                ("index_status", C.c_int32), ("_pad", C.c_uint32)]
+                ("index_status", C.c_int32), ("_pad", C.c_uint32), ("host_ns", C.c_uint64),
+                ("device_ns", C.c_uint64)]
 
 
 # every entry point declared in include/zd.h: name -> (restype, argtypes)
