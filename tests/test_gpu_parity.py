@@ -196,6 +196,30 @@ def test_corrupted_inputs_forked_plan():
     assert stats["ok"] + stats["err_same"] >= 55, stats
 
 
+def test_multi_block_frames_forked_plan():
+    """C5-shaped frames (1 MiB, 8 blocks: Treeless literals, Repeat tables,
+    repeat offsets across blocks) in a plan of 288 sequence blocks, which takes
+    the forked path: K1's Huffman half builds the LUTs a Treeless block reuses
+    (K2, second stream), its sequence half the tables a Repeat block reuses
+    (K3).  Intact parity, then corruptions inside the plan."""
+    parts = [gen.frames(gen.text(20 << 20, seed=21), 1 << 20, 9),
+             gen.frames(gen.xml(8 << 20, seed=22), 1 << 20, 9),
+             gen.frames(gen.binary(8 << 20, seed=23), 1 << 20, 19)]
+    data = b"".join(parts)
+    from zstd_decompressor.batch import frames_index
+    frames, blocks, st, _ = frames_index(data)
+    assert st == 0 and len(frames) == 36 and sum(b["type"] == 2 for b in blocks) >= 256
+    ost, _ = assert_parity(data, False, "multi-block forked plan")
+    assert ost == 0
+    r = random.Random(5)
+    for it in range(8):
+        d = bytearray(data)
+        f = frames[r.randrange(4, 32)]
+        for _ in range(r.randrange(1, 3)):
+            d[f["src_offset"] + r.randrange(f["src_size"])] = r.randrange(256)
+        assert_parity(bytes(d), False, f"multi-block forked corrupt #{it}", allow_ood=True)
+
+
 def test_many_frame_roundtrip_large():
     """Size-independent property at a larger size: decode(compress(x)) == x,
     and the per-frame statuses are all OK."""
