@@ -220,6 +220,33 @@ def test_multi_block_frames_forked_plan():
         assert_parity(bytes(d), False, f"multi-block forked corrupt #{it}", allow_ood=True)
 
 
+def test_parallel_host_walk():
+    """Inputs of >= 4 MiB and >= 512 frames are indexed by threads over frame
+    ranges (zd_host.cpp plan_index); the plan must equal the serial walk's:
+    same first failing frame and status, same output before it.  Corruptions
+    around the range boundaries, in block headers (the header-only pass stops
+    there) and in block contents, and truncations."""
+    src = gen.text(1024 * (16 << 10), seed=31)
+    data = gen.frames(src, 16 << 10, 1)
+    from zstd_decompressor.batch import frames_index
+    frames = frames_index(data)[0]
+    assert len(frames) == 1024 and len(data) >= 4 << 20
+    ost, _ = assert_parity(data, False, "parallel walk, intact")
+    assert ost == 0
+    r = random.Random(9)
+    for it in range(24):
+        d = bytearray(data)
+        k = [63, 64, 127, 128, 255, 256, 511, 512, 700, 1000][it % 10] + r.randrange(-2, 3)
+        f = frames[max(0, min(k, 1023))]
+        if it % 3 == 0:                            # a block header (after the frame header)
+            d[f["src_offset"] + 6 + r.randrange(3)] ^= 1 << r.randrange(8)
+        else:
+            d[f["src_offset"] + r.randrange(f["src_size"])] = r.randrange(256)
+        if it % 8 == 7:
+            d = d[: f["src_offset"] + r.randrange(f["src_size"])]
+        assert_parity(bytes(d), False, f"parallel walk corrupt #{it} (frame {k})", allow_ood=True)
+
+
 def test_many_frame_roundtrip_large():
     """Size-independent property at a larger size: decode(compress(x)) == x,
     and the per-frame statuses are all OK."""

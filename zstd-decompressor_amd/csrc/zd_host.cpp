@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/zd.h"
@@ -342,6 +343,7 @@ namespace {
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 4096;
+constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
 
 // Builds device-side descriptors from the host frames.  `prev_*` seed the
 // Treeless/Repeat resolution (context API), -1 when absent.
@@ -549,14 +551,105 @@ int upload_plan(zd_plan* P) {
   return 0;
 }
 
-int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
-  Bytes in{src, n};
-  while (in.n) {                              // FrameIterator::next (frame.rs:94-99)
+// One frame's extent from its headers alone (magic, frame header, block
+// headers, checksum), without parsing block contents.  false wherever
+// index_frame could fail or the structure is unusual (the walk hands the rest
+// to a serial index).
+bool skip_frame(Bytes& in) {
+  uint64_t magic;
+  if (in.le(4, &magic)) return false;
+  if ((uint32_t)magic == MAGIC_ZSTD) {
+    zd_frame_desc f;
+    memset(&f, 0, sizeof f);
+    if (parse_header(in, &f) || f.window_size > MAX_WIN_SIZE) return false;
+    for (;;) {
+      uint64_t x;
+      if (in.le(3, &x)) return false;
+      const uint32_t type = (x >> 1) & 3, size = (uint32_t)(x >> 3);
+      const uint64_t len = type == 1 ? 1 : size;
+      if (type == 3 || len == 0 || in.n < len) return false;
+      in.p += len; in.n -= len;
+      if (x & 1) break;
+    }
+    if (f.has_checksum) {
+      if (in.n < 4) return false;
+      in.p += 4; in.n -= 4;
+    }
+    return true;
+  }
+  if (((uint32_t)magic ^ MAGIC_SKIP) <= 0x0F) {
+    uint64_t len;
+    if (in.le(4, &len) || len == 0 || in.n < len) return false;
+    in.p += len; in.n -= len;
+    return true;
+  }
+  return false;
+}
+
+// Frames from in (FrameIterator::next, frame.rs:94-99) until the input ends,
+// `limit` frames are indexed, or one fails (kept, with its status).
+int index_frames(const uint8_t* src, Bytes& in, size_t limit, std::vector<HostFrame>& out) {
+  while (in.n && out.size() < limit) {
     HostFrame hf;
     int r = index_frame(src, in, &hf);
-    P->frames.push_back(std::move(hf));
-    if (r) { P->index_status = r; break; }
+    out.push_back(std::move(hf));
+    if (r) return r;
   }
+  return 0;
+}
+
+// The host walk.  Large inputs: a serial header-only pass finds the frame
+// extents, then threads index contiguous frame ranges (the compressed-block
+// headers parsed in parallel); the result is the serial walk's, first failing
+// frame included -- a range that does not end where the next one starts
+// (cannot happen while skip_frame and index_frame agree) falls back to it.
+int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
+  std::vector<size_t> starts;
+  if (n >= PAR_INDEX_MIN_BYTES) {
+    Bytes w{src, n};
+    while (w.n) {
+      const size_t at = (size_t)(w.p - src);
+      if (!skip_frame(w)) break;
+      starts.push_back(at);
+    }
+  }
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t T = std::min<size_t>(hw, starts.size() / 256);
+  if (T >= 2) {
+    std::vector<std::vector<HostFrame>> part(T);
+    std::vector<int> st(T, 0);
+    std::vector<size_t> end(T, 0);
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < T; k++) {
+      const size_t f0 = starts.size() * k / T, f1 = starts.size() * (k + 1) / T;
+      th.emplace_back([&, k, f0, f1] {
+        part[k].reserve(f1 - f0 + 1);
+        Bytes in{src + starts[f0], n - starts[f0]};
+        // the last range runs on past the skipped frames, to the input's end
+        st[k] = index_frames(src, in, k + 1 == T ? SIZE_MAX : f1 - f0, part[k]);
+        end[k] = (size_t)(in.p - src);
+      });
+    }
+    for (auto& t : th) t.join();
+    bool agree = true;
+    for (size_t k = 0; k + 1 < T && agree; k++) {
+      if (st[k]) break;
+      agree = end[k] == starts[starts.size() * (k + 1) / T];
+    }
+    if (agree) {
+      size_t total = 0;
+      for (auto& v : part) total += v.size();
+      P->frames.reserve(total);
+      for (size_t k = 0; k < T; k++) {
+        for (auto& hf : part[k]) P->frames.push_back(std::move(hf));
+        if (st[k]) { P->index_status = st[k]; break; }
+      }
+      P->index_stop = P->frames.size();
+      return 0;
+    }
+  }
+  Bytes in{src, n};
+  P->index_status = index_frames(src, in, SIZE_MAX, P->frames);
   P->index_stop = P->frames.size();
   return 0;
 }
@@ -644,11 +737,16 @@ int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) 
   P->flags = flags;
   const auto t0 = std::chrono::steady_clock::now();
   plan_index(P, src, n);
+  const auto ti = std::chrono::steady_clock::now();
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {1, 4, 8};
   build_plan(P, -1, none, 0, rep0, 0);
   P->info.src_bytes = n;
   const auto t1 = std::chrono::steady_clock::now();
+  if (getenv("ZD_PLAN_TIMES"))
+    fprintf(stderr, "zd plan: index %.2f ms, descriptors %.2f ms\n",
+            std::chrono::duration<double, std::milli>(ti - t0).count(),
+            std::chrono::duration<double, std::milli>(t1 - ti).count());
   int r = upload_plan(P);
   if (r) { zd_plan_destroy(P); return r; }
   const auto t2 = std::chrono::steady_clock::now();
