@@ -70,6 +70,36 @@ def test_fuzz_structure_aware():
     assert seen["ood"] <= max(30, iters // 10), seen
 
 
+def test_fuzz_forked_plans():
+    """The same mutations spliced into the middle of a 300-frame plan.  Plans
+    of 256-4096 frames take the few-frames path: K1's two halves and K2 | K3
+    on two streams, K4F (zd_host.cpp FORK_* / K4F_AUTO_*).  Inputs this size
+    also take the threaded header walk.  ZD_FUZZ_PLAN_ITERS runs longer
+    campaigns (default: 40 inputs)."""
+    from zstd_decompressor.batch import decompress_status, frames_index
+    iters = int(os.environ.get("ZD_FUZZ_PLAN_ITERS", "40"))
+    r = random.Random(int(os.environ.get("ZD_FUZZ_SEED", str(0xF022)), 0) + 1)
+    seeds = _seeds()
+    src = gen.text(300 * 4096, seed=8)
+    base = gen.frames(src, 4096, 3)
+    spans = [(f["src_offset"], f["src_size"]) for f in frames_index(base)[0]]
+    assert len(spans) == 300
+    seen = {"ok": 0, "err": 0, "ood": 0}
+    for it in range(iters):
+        o, n = spans[r.randrange(16, 284)]
+        data = base[:o] + _mutate(r, seeds) + base[o + n:]
+        p = r.random() < 0.3
+        ost, oout = oracle.decompress_status(data, p)
+        gst, gout = decompress_status(data, p)
+        if gst == OUT_OF_DOMAIN:
+            seen["ood"] += 1
+            continue
+        assert gst == ost, f"#{it}: oracle {ost}, gpu {gst}"
+        assert gout == oout, f"#{it}: output differs"
+        seen["ok" if ost == 0 else "err"] += 1
+    assert seen["ood"] <= max(8, iters // 10), seen
+
+
 # (seed, input index) of campaign inputs that once disagreed with the oracle
 REGRESSIONS = [
     (6, 4281),   # runaway Huffman-weight stream before a reserved sequence-mode bit: oracle REF_PANIC
