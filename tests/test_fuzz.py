@@ -72,7 +72,7 @@ def test_fuzz_structure_aware():
 
 def test_fuzz_forked_plans():
     """The same mutations spliced into the middle of a 300-frame plan.  Plans
-    of 256-4096 frames take the few-frames path: K1's two halves and K2 | K3
+    of 256-768 frames take the few-frames path: K1's two halves and K2 | K3
     on two streams, K4F (zd_host.cpp FORK_* / K4F_AUTO_*).  Inputs this size
     also take the threaded header walk.  ZD_FUZZ_PLAN_ITERS runs longer
     campaigns (default: 40 inputs)."""

@@ -173,7 +173,7 @@ def test_corrupted_inputs():
 
 
 def test_corrupted_inputs_forked_plan():
-    """Corruptions inside a 300-frame plan: plans of 256-4096 frames take the
+    """Corruptions inside a 300-frame plan: plans of 256-768 frames take the
     few-frames path (K1's Huffman half + K2 on a second stream beside K1's
     sequence half + K3, then K4F; zd_host.cpp FORK_* / K4F_AUTO_*), whose
     error keys come from both streams.  Same first error and partial output

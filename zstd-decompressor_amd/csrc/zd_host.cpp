@@ -342,7 +342,11 @@ namespace {
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 4096;
+// K4F takes one workgroup per CU: rounds of 256 frames at ~0.21 ms each
+// against the streaming K4's one round (~0.75 ms) up to 4096 frames, so it
+// pays for up to three rounds (scripts/exp_thresholds.sh: 8192 frames 12.1
+// vs 7.7 ms per step)
+constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 3 * 256;
 constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
 
 // Builds device-side descriptors from the host frames.  `prev_*` seed the
@@ -461,7 +465,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     fd.out = out_off;
     fd.out_cap = cap;
     // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
-    // executes the frames that fit it in plans of 256-4096 frames, where the
+    // executes the frames that fit it in plans of 256-768 frames, where the
     // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
     // it is slower on C4.  ZD_K4F=1 / 0 forces it on / off.
     fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
@@ -527,7 +531,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   return 0;
 }
 
-constexpr size_t FORK_MAX_SEQ_BLOCKS = 256 * 16;   // MI355X CUs x K3 chains per workgroup
+// K2 | K3 fork while K3 needs at most two workgroups per CU (256 CUs x 16
+// chains each): 8192 blocks 7.73 -> 7.40 ms per step, 16384 blocks 8.94 ->
+// 10.01 (scripts/exp_thresholds.sh)
+constexpr size_t FORK_MAX_SEQ_BLOCKS = 2 * 256 * 16;
 constexpr size_t FORK_MIN_SEQ_BLOCKS = 256;
 
 int upload_plan(zd_plan* P) {
@@ -822,7 +829,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
   // K2 beside K3 on a second stream: measured slower on C4 (61.4 vs 57.9 ms:
   // K3 is LDS-bound and K2 takes its CUs), so it is taken only when K3's
-  // chains use at most one workgroup per CU (<= 256 x 16 blocks: the few-
+  // chains use at most two workgroups per CU (FORK_MAX_SEQ_BLOCKS: the few-
   // frames regime, where both kernels run one round at their chain latency)
   // and there are enough of them for the overlap to pay for a second stream;
   // ZD_FORK=1 / 0 forces it on / off
