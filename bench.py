@@ -1,15 +1,23 @@
 """Benchmark: decompressed MB/s of the MI355X ZSTD block-decode path.
 
-Workload (default `c4`, BASELINE.json configs[3] at one GPU's share):
-enwik-style synthetic text, 128 KiB independent frames at zstd level 3,
-a 1 GiB unique frame set replicated to 10 GiB decompressed per GPU
-(SURVEY.md §8d allows replication).  One step = one zd_decode_async over the
-whole resident corpus (K1 tables -> K2 Huffman -> K3 FSE -> K4 execute).
-Inputs are resident in HBM before timing; output is verified bit-exact
-against the source bytes after timing.
+Workload (default `c4`, BASELINE.json configs[3]): enwik-style synthetic
+text, 128 KiB independent frames at zstd level 3, a 1 GiB unique frame set
+replicated to one 10 GiB corpus (SURVEY.md §8d allows replication).  One
+step = one zd_decode_async over the whole resident share (K1 tables -> K2
+Huffman -> K3 FSE -> K4 execute).  Inputs are resident in HBM before timing;
+output is verified bit-exact against the source bytes after timing.
 
-Multi-GPU: one process per GPU (torchrun), each rank decodes its own
-10 GiB shard — independent frames, no data-path collective (scaling "weak").
+Multi-GPU (torchrun, one process per GPU): by default the one 10 GiB corpus
+is split into contiguous frame ranges balanced by compressed bytes
+(shard.partition, zd_shard_partition), each rank planning and decoding only
+its range — no data-path collective ("scaling": "strong", value = all
+ranks' bytes / the slowest rank's time).  The gather of every rank's output
+to rank 0 over RCCL (libzd's zd_comm_gather) is timed after that and
+reported apart.  `--scaling weak` gives every rank its own 10 GiB corpus.
+
+Other workloads: c2 (one 64 MiB raw/RLE frame), c3 (enwik8 shape in 763
+frames), c3s (the same 100,000,000 bytes as ONE frame, `zstd -3 enwik8`:
+block-parallel executor K4J), c5 (1 MiB eight-block frames, --level 1/9/19).
 """
 from __future__ import annotations
 
@@ -35,8 +43,8 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_corpus(workload: str, unique_bytes: int, seed: int):
-    from corpus import gen
+def make_corpus(workload: str, unique_bytes: int, seed: int, level: int = 9):
+    from corpus import gen, libzstd
     t0 = time.time()
     if workload == "c2":
         data, src = gen.c2_raw_rle(64 << 20, with_content=True)
@@ -48,13 +56,57 @@ def make_corpus(workload: str, unique_bytes: int, seed: int):
         src = gen.text(100_000_000, seed=seed)[:100_000_000]
         data = gen.frames(src, 128 << 10, 3)
         return data, src, 1, {"frame_bytes": 128 << 10, "level": 3}, time.time() - t0
+    if workload == "c3s":
+        # the same 100,000,000 bytes as the stock CLI writes them: ONE frame
+        # (763 blocks, windowLog 21), executed block-parallel (K4J)
+        src = gen.text(100_000_000, seed=seed)[:100_000_000]
+        data = libzstd.compress(src, 3)
+        return data, src, 1, {"frames": 1, "level": 3}, time.time() - t0
     if workload == "c5":
         src = gen.text(unique_bytes, seed=seed)
-        data = gen.frames(src, 1 << 20, 9)
-        return data, src, None, {"frame_bytes": 1 << 20, "level": 9}, time.time() - t0
+        data = gen.frames(src, 1 << 20, level)
+        return data, src, None, {"frame_bytes": 1 << 20, "level": level}, time.time() - t0
     src = gen.text(unique_bytes, seed=seed)
     data = gen.frames(src, 128 << 10, 3)
     return data, src, None, {"frame_bytes": 128 << 10, "level": 3}, time.time() - t0
+
+
+def host_cores():
+    """(threads for the CPU baseline, note).  BASELINE.md §3 asks for every host
+    core; a container's share can be smaller than os.cpu_count() (the GPU box
+    shows the whole machine there), so the cores this process may run on
+    (affinity, then a cgroup v2 CPU quota) bound it."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    note = f"os.cpu_count()={os.cpu_count()}, affinity={n}"
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+            note += f", cgroup cpu.max quota={quota}"
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    return max(1, n), note
+
+
+def shard_bytes(frame_set: bytes, frames, src, reps: int, begin: int, end: int):
+    """The compressed bytes and the source bytes of global frames [begin, end)
+    of `frame_set` replicated `reps` times (frame k = frame k % F of the set)."""
+    F = len(frames)
+    coff = [0]
+    for f in frames:
+        coff.append(coff[-1] + f["content_size"])
+    data, ref = [], []
+    k = begin
+    while k < end:
+        i = k % F
+        run = min(end - k, F - i)                      # contiguous inside one replica
+        a, b = frames[i]["src_offset"], frames[i + run - 1]["src_offset"] + frames[i + run - 1]["src_size"]
+        data.append(frame_set[a:b])
+        if src is not None:
+            ref.append(src[coff[i]:coff[i + run]])
+        k += run
+    return b"".join(data), (b"".join(ref) if src is not None else None)
 
 
 def cpu_baseline(frame_set: bytes, threads: int, budget_s: float = 20.0):
@@ -136,11 +188,12 @@ def cpu_libzstd(frame_set: bytes, sample, threads: int):
                       f"{L.ZSTD_versionNumber()} ZSTD_decompress on {threads} host threads, {dt:.2f} s"}
 
 
-def traffic_of(kernel: str, args):
+def traffic_of(kernel: str, args, world: int):
     """HBM bytes per launch of `kernel` (FETCH_SIZE + WRITE_SIZE, rocprofv3
-    --pmc passes of scripts/full_run.sh on the default workload, kept in
-    profiles/traffic.json); None for other workloads or when absent."""
-    if (args.workload, args.unique_mib, args.replicas) != ("c4", 1024, 10):
+    --pmc passes of scripts/full_run.sh on the default 1-GPU workload, kept
+    with the commit they measured in profiles/traffic.json); None for other
+    workloads or when absent."""
+    if (args.workload, args.unique_mib, args.replicas, world) != ("c4", 1024, 10, 1):
         return None
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
@@ -155,16 +208,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "c3", "c5"])
-    ap.add_argument("--unique-mib", type=int, default=1024, help="unique decompressed MiB per rank before replication")
+    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "c3", "c3s", "c5"])
+    ap.add_argument("--level", type=int, default=9, help="c5: zstd level (1 / 9 / 19)")
+    ap.add_argument("--unique-mib", type=int, default=1024, help="unique decompressed MiB before replication")
     ap.add_argument("--replicas", type=int, default=10)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="N>1: one corpus split across the ranks (strong) or one corpus per rank (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use")
     ap.add_argument("--corpus-cache", default=os.environ.get("ZD_CORPUS_CACHE"),
                     help="directory to keep the generated corpus in between runs (experiments)")
-    ap.add_argument("--gather", action="store_true",
-                    help="N>1: also time gathering every rank's output to rank 0 (SURVEY §8e), reported apart")
+    ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
+                    help="N>1: time gathering every rank's output to rank 0 over RCCL, reported apart "
+                         "(auto: on for strong scaling)")
     ap.add_argument("--experiment", action="store_true",
                     help="timing-only variants: do not stop on decode errors")
     args = ap.parse_args()
@@ -179,36 +236,48 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    import zstd_decompressor as zd
-    from zstd_decompressor.batch import Plan
+    import zstd_decompressor as zd  # noqa: F401
+    from zstd_decompressor import shard
+    from zstd_decompressor.batch import Plan, frames_index
 
-    # ---- corpus (host), one unique frame set per rank ----
-    seed = 0x5EED + 7919 * rank
+    # ---- corpus (host) ----
+    strong = world > 1 and args.scaling == "strong" and args.workload != "c3s"
+    seed = 0x5EED + (0 if (strong or world == 1) else 7919 * rank)
     cache = None
     if args.corpus_cache:
         os.makedirs(args.corpus_cache, exist_ok=True)
-        cache = os.path.join(args.corpus_cache, f"{args.workload}_{args.unique_mib}_{seed}")
+        lv = f"_L{args.level}" if args.workload == "c5" else ""
+        cache = os.path.join(args.corpus_cache, f"{args.workload}{lv}_{args.unique_mib}_{seed}")
     if cache and os.path.exists(cache + ".zst"):
         frame_set = open(cache + ".zst", "rb").read()
         src = open(cache + ".src", "rb").read() if os.path.exists(cache + ".src") else None
-        reps_override, tgen = (1 if args.workload in ("c2", "c3") else None), 0.0
+        reps_override, tgen = (1 if args.workload in ("c2", "c3", "c3s") else None), 0.0
     else:
-        frame_set, src, reps_override, meta, tgen = make_corpus(args.workload, args.unique_mib << 20, seed)
+        frame_set, src, reps_override, meta, tgen = make_corpus(args.workload, args.unique_mib << 20, seed, args.level)
         if cache:
             open(cache + ".zst", "wb").write(frame_set)
             if src is not None:
                 open(cache + ".src", "wb").write(src)
     reps = reps_override or args.replicas
-    data = frame_set * reps
-    log(f"[rank {rank}] corpus: {len(frame_set) / 2**20:.1f} MiB compressed x{reps}, gen {tgen:.1f}s")
+    set_frames = frames_index(frame_set)[0]
+    n_global = len(set_frames) * reps
+    if strong:
+        # one corpus, contiguous frame ranges balanced by compressed bytes
+        ranges = shard.partition([set_frames[k % len(set_frames)]["src_size"] for k in range(n_global)], world)
+        fb, fe = ranges[rank]
+        data, ref_bytes = shard_bytes(frame_set, set_frames, src, reps, fb, fe)
+    else:
+        fb, fe = 0, n_global
+        data, ref_bytes = frame_set * reps, None
+    log(f"[rank {rank}] corpus: {len(frame_set) / 2**20:.1f} MiB compressed x{reps}, gen {tgen:.1f}s; "
+        f"this rank: frames [{fb}, {fe}) of {n_global}, {len(data) / 2**20:.1f} MiB")
 
     # the host plan (frame/block header walk, descriptors, workspace
     # allocation and upload) is built once per input, outside the timed
     # region; its wall time is reported beside value as host_plan_ms
     # (a plan over the first frame first: HIP runtime / code-object set-up is
     # a one-time process cost, not part of planning an input)
-    from zstd_decompressor.batch import frames_index
-    f0 = frames_index(frame_set, 1)[0][0]
+    f0 = set_frames[0]
     Plan(frame_set[f0["src_offset"]:f0["src_offset"] + f0["src_size"]]).close()
     t0 = time.time()
     plan = Plan(data)
@@ -269,32 +338,25 @@ def main():
     verified = None
     if not args.no_verify and src is not None:
         st, total, _, _, _ = plan.results(d_dst.data_ptr(), sptr)
-        ref = torch.frombuffer(bytearray(src), dtype=torch.uint8).to(dev)
-        u = len(src)
-        ok = st == 0 and total == u * reps
-        for r in range(reps):
-            ok = ok and bool(torch.equal(d_dst[r * u:(r + 1) * u], ref))
+        ok = st == 0 and total == info.out_bytes
+        if strong:
+            ref = torch.frombuffer(bytearray(ref_bytes), dtype=torch.uint8).to(dev)
+            ok = ok and total == ref.numel() and bool(torch.equal(d_dst[:total], ref))
+        else:
+            ref = torch.frombuffer(bytearray(src), dtype=torch.uint8).to(dev)
+            u = len(src)
+            ok = ok and total == u * reps
+            for r in range(reps):
+                ok = ok and bool(torch.equal(d_dst[r * u:(r + 1) * u], ref))
         verified = bool(ok)
         del ref
+        if dist:
+            v = torch.tensor([1 if verified else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(v, op=dist.ReduceOp.MIN)
+            verified = bool(v.item())
         assert args.experiment or verified, "GPU output differs from the source bytes"
 
-    # ---- optional: gather of the decoded frames to rank 0 (never part of value) ----
-    gather = None
-    if dist and args.gather:
-        from zstd_decompressor import shard
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.time()
-        got = shard.gather_to_root(d_dst, info.out_bytes, rank, world)
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        tg = torch.tensor([time.time() - tg], dtype=torch.float64, device=dev)
-        dist.all_reduce(tg, op=dist.ReduceOp.MAX)
-        gb = float(info.out_bytes) * world
-        gather = {"gather_ms": round(tg.item() * 1e3, 3),
-                  "decode_plus_gather_MBps": round(gb / (ms_per_step / 1e3 + tg.item()) / 1e6, 1)}
-        del got
-
+    # ---- gather of the decoded ranges to rank 0 over RCCL (never part of value) ----
     out_bytes = info.out_bytes
     comp_bytes = len(data)
     total_out = torch.tensor([float(out_bytes)], dtype=torch.float64, device=dev)
@@ -302,6 +364,41 @@ def main():
     if dist:
         dist.all_reduce(total_out)
         dist.all_reduce(total_alg)
+    gather = None
+    if dist and (args.gather == "on" or (args.gather == "auto" and strong)):
+        comm = shard.Comm(rank, world, dev)
+        all_out = int(total_out.item())
+        root = torch.empty(all_out + 64 if rank == 0 else 1, dtype=torch.uint8, device=dev)
+        gst = None
+        tg = []
+        for it in range(3):                           # one warm-up, two timed
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.time()
+            cst, res = comm.gather(d_dst.data_ptr(), out_bytes, 0, -1, root.data_ptr(), all_out if rank == 0 else 0,
+                                   sptr)
+            torch.cuda.synchronize(dev)
+            dt = torch.tensor([time.time() - t1], dtype=torch.float64, device=dev)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            if it:
+                tg.append(dt.item())
+            gst = (cst, res.status, res.total_len)
+        gms = min(tg) * 1e3
+        gok = None
+        if rank == 0 and not args.no_verify and src is not None:
+            ref = torch.frombuffer(bytearray(src), dtype=torch.uint8).to(dev)
+            u = len(src)
+            gok = gst[0] == 0 and gst[1] == 0 and gst[2] == u * reps and all(
+                bool(torch.equal(root[r * u:(r + 1) * u], ref)) for r in range(reps))
+            del ref
+        gather = {"gather_ms": round(gms, 3), "gathered_bytes": int(gst[2]),
+                  "gather_GBps": round(gst[2] / (gms / 1e3) / 1e9, 1),
+                  "decode_plus_gather_MBps": round(all_out / (ms_per_step / 1e3 + gms / 1e3) / 1e6, 1),
+                  "via": "libzd zd_comm_gather (RCCL point-to-point to rank 0 over xGMI)",
+                  "verified_bit_exact": gok}
+        del root
+        comm.close()
+
     value = total_out.item() / (ms_per_step / 1e3) / 1e6
     alg_per_launch = out_bytes + comp_bytes          # C + D, this rank's launch
     dom_ms = kt[dom]
@@ -309,14 +406,24 @@ def main():
 
     cpu = cpu_zstd = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and src is not None:
-        threads = min(args.cpu_threads, os.cpu_count() or 1)
+        threads, note = host_cores()
+        if args.cpu_threads:
+            threads = args.cpu_threads
         cpu, sample = cpu_baseline(frame_set, threads)
+        cpu["cores_note"] = note
         try:
             cpu_zstd = cpu_libzstd(frame_set, sample, threads)
         except Exception as ex:                     # context only: never fails the bench
             cpu_zstd = {"error": str(ex)[:200]}
 
     if rank == 0:
+        wl = {"c4": "C4: enwik-style text, 128 KiB frames, zstd -3, 1 GiB unique x10 = one 10 GiB corpus",
+              "c2": "C2: single 64 MiB frame, 512 alternating raw/RLE 128 KiB blocks",
+              "c3": "C3: enwik8-style 100,000,000 B, 763 x 128 KiB frames, zstd -3",
+              "c3s": "C3 single frame: enwik8-style 100,000,000 B as ONE zstd -3 frame (763 blocks)",
+              "c5": f"C5: text, 1 MiB multi-block frames, zstd -{args.level}"}[args.workload]
+        if world > 1:
+            wl += (f", frame-sharded across {world} GPUs" if strong else f", one such corpus per GPU ({world})")
         res = {
             "metric": "decompressed MB/s (bit-exact vs ref) + % HBM roofline",
             "value": round(value, 1),
@@ -326,20 +433,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": {"c4": "C4: enwik-style text, 128 KiB frames, zstd -3, 1 GiB unique x10 per GPU",
-                             "c2": "C2: single 64 MiB frame, 512 alternating raw/RLE 128 KiB blocks",
-                             "c3": "C3: enwik8-style 100,000,000 B, 763 x 128 KiB frames, zstd -3",
-                             "c5": "C5: text, 1 MiB multi-block frames, zstd -9"}[args.workload],
-                "frames_per_gpu": int(info.nframes),
-                "decompressed_bytes_per_gpu": int(out_bytes),
-                "compressed_bytes_per_gpu": int(comp_bytes),
-                "sequences_per_gpu": int(info.nsequences),
-                "parallelism": f"frame-sharded x{world}",
+                "workload": wl,
+                "frames_total": int(n_global) if strong else int(info.nframes) * world,
+                "frames_rank0": int(info.nframes),
+                "decompressed_bytes_total": int(total_out.item()),
+                "decompressed_bytes_rank0": int(out_bytes),
+                "compressed_bytes_rank0": int(comp_bytes),
+                "sequences_rank0": int(info.nsequences),
+                "parallelism": f"frame-sharded x{world}" if strong else f"replicas x{world}",
             },
             "roofline": {
                 "bound": "hbm",
@@ -348,7 +454,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic_of(dom, args),
+                "traffic": traffic_of(dom, args, world),
                 "traffic_unit": "GB per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, profiles/traffic.json)",
                 "alg_bytes_per_launch": int(alg_per_launch),
                 "pipeline_achieved": round(alg_per_launch / (ms_per_step / 1e3) / 1e9, 1),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 2
+#define ZD_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -73,6 +73,7 @@ extern "C" {
 #define ZD_E_HIP             (-94) /* a HIP runtime call failed */
 #define ZD_E_NO_MEMORY       (-95)
 #define ZD_E_NOT_DECODED     (-96) /* frame skipped: an earlier frame failed (FrameIterator stops, frame.rs:94-99) */
+#define ZD_E_COMM            (-97) /* an RCCL call failed, or RCCL is not loadable */
 
 /* Human-readable name of a status code (static storage). */
 const char* zd_status_name(int status);
@@ -137,6 +138,10 @@ int zd_frames_index(const uint8_t* src, size_t n,
 typedef struct zd_plan zd_plan;
 
 #define ZD_F_SKIPPABLE  1u  /* append skippable-frame payloads to the output (CLI -p, src/main.rs:45-48) */
+/* Executor choice for frames of many blocks; default:
+ * automatic.  Same output either way; tests run both. */
+#define ZD_F_BLOCK_PARALLEL 2u  /* every frame with a compressed block -> K4J (block-parallel execute) */
+#define ZD_F_FRAME_SERIAL   4u  /* no frame -> K4J (the streaming per-frame executor) */
 
 typedef struct zd_plan_info {
   uint64_t nframes;        /* frames in the plan (skippable included) */
@@ -204,6 +209,65 @@ int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, 
  * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
 int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
                   size_t* out_len, uint32_t flags);
+
+/* ------------------------------------------------------------------ */
+/* Multi-GPU: frame-range sharding + RCCL gather.      */
+/* Frames are independent (a fresh DecodingContext each, frame.rs:     */
+/* 232-237) and the CLI concatenates their outputs, stopping at the    */
+/* first failing frame (src/main.rs:43-53).  One process per GPU; each */
+/* rank decodes a contiguous frame range into its own HBM (no data-    */
+/* path collective), then the ranges are gathered to rank 0.           */
+/* ------------------------------------------------------------------ */
+
+/* Contiguous frame ranges balanced by compressed bytes: rank k takes
+ * frames [cuts[k], cuts[k+1]) (cuts has world + 1 entries; every rank gets a
+ * frame while there are at least `world`).  Host only. */
+int zd_shard_partition(const uint64_t* frame_bytes, size_t nframes, int world, size_t* cuts);
+
+/* Rank's share of src: byte range [*src_begin, *src_end) and frame range
+ * (frames indexed on the host with zd_frames_index).  A frame that fails
+ * to index and the rest of the input go to the last rank, whose plan then
+ * reports it.  Host only. */
+int zd_shard_range(const uint8_t* src, size_t n, int rank, int world, uint64_t* src_begin, uint64_t* src_end,
+                   uint64_t* frame_begin, uint64_t* frame_end);
+
+typedef struct zd_comm zd_comm;
+#define ZD_COMM_ID_BYTES 128
+
+/* An RCCL communicator over `world` ranks, one GPU each (the calling
+ * thread's current HIP device).  Rank 0 makes the id and shares it out of
+ * band (e.g. a torch.distributed broadcast); every rank then calls
+ * zd_comm_create with it.  RCCL is loaded on first use. */
+int zd_comm_unique_id(uint8_t id[ZD_COMM_ID_BYTES]);
+int zd_comm_create(const uint8_t id[ZD_COMM_ID_BYTES], int world, int rank, zd_comm** out);
+void zd_comm_destroy(zd_comm* comm);
+
+typedef struct zd_gather_result {
+  uint64_t total_len;         /* bytes gathered on rank 0 */
+  int32_t status;             /* the whole input's status: the first failing rank's */
+  int32_t failed_rank;        /* that rank, or world when none failed */
+  int64_t first_error_frame;  /* global index of the first failing frame, -1 if none */
+} zd_gather_result;
+
+/* Collective (every rank calls it): each rank's outcome — status, first
+ * failing frame (global index), decoded length — is all-gathered; the output
+ * stops at the first failing rank's failure (its frames before the failure
+ * kept, later ranks contribute nothing), and rank 0 receives the ranks'
+ * d_local bytes in rank order at d_root_out (capacity root_cap; rank 0's own
+ * bytes are copied unless d_local == d_root_out) with RCCL point-to-point
+ * transfers on `stream`.  The same *res on every rank.  ZD_E_DST_TOO_SMALL
+ * (on every rank, nothing sent) when rank 0's capacity is short. */
+int zd_comm_gather(zd_comm* comm, const uint8_t* d_local, uint64_t local_len, int32_t status,
+                   int64_t first_error_frame, uint8_t* d_root_out, uint64_t root_cap, zd_gather_result* res,
+                   void* stream);
+
+/* The whole multi-GPU decode (the reference's `decode every frame of a
+ * file`, sharded): every rank passes the same host input; rank `comm`'s
+ * frame range is planned, copied to HBM, decoded, and gathered to rank 0
+ * (zd_comm_gather).  Returns the local call's status (ZD_OK when the
+ * collective completed); the input's status is res->status. */
+int zd_decode_sharded(zd_comm* comm, const uint8_t* src, size_t n, uint32_t flags, uint8_t* d_root_out,
+                      uint64_t root_cap, zd_gather_result* res, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* DecodingContext mirror (decoding_context.rs:17-106): GPU-resident    */

@@ -21,7 +21,8 @@ run() {  # name seconds cmd...
 for s in "$@"; do
   case "$s" in
     build) run build 300 python -c "import __graft_entry__ as g; g.build()" || exit 1 ;;
-    test)  run pytest 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    test)  run pytest 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    large) run pytest_large 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread tests/test_large_frames.py tests/test_resource_digests.py "tests/test_gpu_parity.py::test_hip_graph_capture_replay" ;;
     testall) run pytest_all 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;

@@ -350,3 +350,46 @@ def test_k2_deep_trees_beside_libzstd_frames():
     assert ost == 0
     for i, f in enumerate(deep_err[:8]):
         assert_parity(f, False, f"deep tree, rejected #{i}")
+
+
+@pytest.mark.parametrize("shape", ["one_frame", "forked_300_frames", "block_parallel"])
+def test_hip_graph_capture_replay(shape):
+    """zd_decode_async is graph-safe (include/zd.h): no allocation, no host
+    memory read (states reset from device-resident copies), the second
+    stream made at plan time.  Capture it in a HIP graph, clear the output,
+    replay: same bytes as the source."""
+    import torch
+    from zstd_decompressor import _lib
+    from zstd_decompressor.batch import Plan
+    flags = 0
+    if shape == "one_frame":
+        src = gen.text(1 << 20, seed=61)
+        data = libzstd.compress(src, 3)
+    elif shape == "forked_300_frames":
+        src = gen.text(300 * 4096, seed=62)
+        data = gen.frames(src, 4096, 3)
+    else:
+        src = gen.text(3 << 20, seed=63)
+        data = gen.frames(src, 1 << 20, 9)
+        flags = _lib.F_BLOCK_PARALLEL
+    plan = Plan(data, False, flags)
+    n = plan.info.out_bytes
+    dev = torch.device("cuda", 0)
+    d_src = torch.zeros(len(data) + 64, dtype=torch.uint8, device=dev)
+    d_src[: len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    d_dst = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):          # warm-up outside the capture
+        plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), n, s.cuda_stream)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), n, s.cuda_stream)
+    d_dst.zero_()
+    torch.cuda.synchronize(dev)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    st, total, _, _, _ = plan.results(d_dst.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    assert st == 0 and total == len(src)
+    assert bytes(d_dst[:total].cpu().numpy().tobytes()) == src
+    plan.close()

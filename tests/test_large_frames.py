@@ -1,0 +1,121 @@
+"""Single frames of many blocks: the block-parallel executor K4J (pointer
+jumping, zd_kernels.hip KJ1-KJ4) against the oracle and the streaming
+per-frame executor, and frames above 128 MiB.
+
+The reference decodes any frame whose window is at most 8 MiB
+(frame.rs:44,167-169,201-206), with the whole frame as history
+(decoding_context.rs:29-47, block.rs:90-96).  A stock `zstd` run over a big
+file writes exactly one such frame (libzstd level 3: windowLog 21), so the
+shapes here are `zstd -3 enwik8` (100 MB, 763 blocks) and a frame past the
+128 MiB the GPU path used to refuse.  Same output and the same reference
+error variant as the oracle; both executors (plan flags ZD_F_BLOCK_PARALLEL /
+ZD_F_FRAME_SERIAL) on the same bytes.
+"""
+import random
+
+import pytest
+
+from corpus import gen, libzstd
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+OUT_OF_DOMAIN = -91
+
+
+def _gpu(data, flags=0):
+    from zstd_decompressor.batch import decompress_status
+    return decompress_status(data, False, flags)
+
+
+def _flags():
+    from zstd_decompressor import _lib
+    return _lib.F_BLOCK_PARALLEL, _lib.F_FRAME_SERIAL
+
+
+def _parity(data, flags, what, allow_ood=False):
+    ost, oout = oracle.decompress_status(data, False)
+    gst, gout = _gpu(data, flags)
+    if allow_ood and gst == OUT_OF_DOMAIN:
+        return ost, gst
+    if ost == 0:
+        assert gst == 0, f"{what}: oracle ok, gpu status {gst}"
+        assert gout == oout, f"{what}: output differs ({len(gout)} vs {len(oout)} bytes)"
+    else:
+        assert gst == ost, f"{what}: oracle status {ost}, gpu status {gst}"
+        assert gout == oout, f"{what}: partial output differs"
+    return ost, gst
+
+
+@pytest.mark.parametrize("kind", ["text", "xml", "binary"])
+@pytest.mark.parametrize("level", [1, 9, 19])
+def test_block_parallel_multi_block_frames(kind, level):
+    """C5-shaped frames (1 MiB, 8 blocks: Treeless literals, Repeat tables,
+    repeat offsets and matches across blocks) through K4J, forced."""
+    bp, fs = _flags()
+    n = (2 << 20) if level < 19 else (1 << 20)
+    src = {"text": gen.text, "xml": gen.xml, "binary": gen.binary}[kind](n, seed=40 + level)
+    data = gen.frames(src, 1 << 20, level)
+    ost, _ = _parity(data, bp, f"K4J {kind} L{level}")
+    assert ost == 0
+    assert _gpu(data, fs) == (0, src)
+
+
+def test_block_parallel_small_and_raw_rle_frames(kat):
+    """Every frame through K4J: the reference's KAT frames, tiny frames, raw and
+    RLE blocks between compressed ones (C2), checksums, period-1/2 matches."""
+    bp, _ = _flags()
+    for c in kat["frames"]:
+        _parity(bytes(c["data"]), bp, c["src"])
+    for n in (1, 3, 17, 1000, 70000):
+        src = bytes(random.Random(n).randrange(256) for _ in range(n))
+        _parity(libzstd.compress(src, 3), bp, f"tiny {n}")
+    _parity(libzstd.compress(b"a" * 300000, 3), bp, "rle")
+    _parity(libzstd.compress(b"ab" * 300000, 19), bp, "period-2")
+    _parity(gen.c2_raw_rle(4 << 20), bp, "c2 raw/rle")
+    src = gen.text(600_000, seed=7)
+    _parity(gen.frames(src, 300_000, 3, checksum=True), bp, "checksum")
+
+
+def test_block_parallel_corrupted_inputs():
+    """Corruptions of multi-block frames through K4J: the first failing
+    sequence of the frame decides the error, as in the reference's in-order
+    decode (the blocks after it ran in parallel and must not change that)."""
+    bp, _ = _flags()
+    r = random.Random(4321)
+    base = gen.frames(gen.text(3 << 20, seed=13), 1 << 20, 9) + gen.frames(gen.binary(1 << 20, seed=14), 1 << 20, 19)
+    stats = {"ok": 0, "err": 0, "ood": 0}
+    for it in range(150):
+        d = bytearray(base)
+        for _ in range(r.randrange(1, 4)):
+            d[r.randrange(len(d))] = r.randrange(256)
+        if r.random() < 0.15:
+            d = d[: r.randrange(len(d))]
+        ost, gst = _parity(bytes(d), bp, f"K4J corrupt #{it}", allow_ood=True)
+        stats["ok" if ost == 0 else ("ood" if gst == OUT_OF_DOMAIN else "err")] += 1
+    assert stats["ok"] + stats["err"] >= 140, stats
+
+
+def test_single_frame_enwik8_shape():
+    """`zstd -3` of a 100,000,000-byte enwik-style text: one frame, 763
+    blocks, windowLog 21 (BASELINE.json configs[2] as a single file)."""
+    from zstd_decompressor.batch import frames_index
+    src = gen.text(100_000_000, seed=8)
+    data = libzstd.compress(src, 3)
+    frames, blocks, st, _ = frames_index(data)
+    assert st == 0 and len(frames) == 1 and len(blocks) > 700
+    assert oracle.decompress(data) == src
+    gst, gout = _gpu(data)                            # automatic: K4J
+    assert gst == 0 and gout == src
+
+
+def test_single_frame_over_128MiB():
+    """A single libzstd frame of 160 MiB (windowLog 21): decoded by K4J
+    (automatic) and by the streaming executor (forced; int32 positions reach
+    2 GiB), both bit-exact against the source and the oracle."""
+    _, fs = _flags()
+    src = gen.text(160 << 20, seed=9)
+    data = libzstd.compress(src, 3)
+    assert oracle.decompress(data) == src
+    assert _gpu(data) == (0, src)
+    assert _gpu(data, fs) == (0, src)

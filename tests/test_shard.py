@@ -28,6 +28,35 @@ def test_partition_covers_and_balances():
     assert rs[0][0] == 0 and rs[-1][1] == 2 and sum(e - b for b, e in rs) == 2
 
 
+def test_native_partition_matches():
+    """zd_shard_partition (the C ABI a host binding calls) cuts exactly where
+    shard.partition does; zd_shard_range gives shard_of's byte ranges."""
+    import random
+    import ctypes as C
+    from zstd_decompressor import _lib
+    r = random.Random(3)
+    for trial in range(300):
+        n = r.randrange(0, 40)
+        sizes = [r.choice([1, 2, 3, 100, 5000, 1 << 20, 1 << 33]) for _ in range(n)]
+        for world in (1, 2, 3, 4, 7, 8):
+            assert shard.partition_native(sizes, world) == shard.partition(sizes, world), (sizes, world)
+    from corpus import gen
+    from zstd_decompressor.batch import frames_index
+    data = gen.frames(gen.text(3 << 20, seed=2), 100_000, 1)
+    frames = frames_index(data)[0]
+    p, n, keep = _lib.buf(data)
+    for world in (1, 3, 8):
+        for rank in range(world):
+            v = [C.c_uint64() for _ in range(4)]
+            _lib.check(_lib.lib().zd_shard_range(p, n, rank, world, *[C.byref(x) for x in v]))
+            assert tuple(x.value for x in v) == shard.shard_of(frames, rank, world)
+    # a frame that fails to index: it and the rest of the input go to the last rank
+    bad = data[: frames[20]["src_offset"]] + b"\x00\x01\x02\x03" + data[frames[20]["src_offset"]:]
+    v = [C.c_uint64() for _ in range(4)]
+    _lib.check(_lib.lib().zd_shard_range(*_lib.buf(bad)[:2], 2, 3, *[C.byref(x) for x in v]))
+    assert v[1].value == len(bad) and v[3].value == 20
+
+
 def test_shard_of_real_frames():
     from corpus import gen
     from zstd_decompressor.batch import frames_index
@@ -92,6 +121,46 @@ def test_gather_to_root_gloo(world):
     assert got == b"".join(payloads)
 
 
+def _worker_fail(rank, world, port, payloads, statuses, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = payloads[rank]
+        st, first = statuses[rank]
+        local = torch.frombuffer(bytearray(mine + b"\x55" * 5), dtype=torch.uint8)
+        gst, gfirst, n, out = shard.collect(local, len(mine), st, first, rank, world)
+        q.put((rank, gst, gfirst, n, None if out is None else bytes(out.numpy().tobytes())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collect_stops_at_first_failing_rank():
+    """A failure on a middle rank: every rank reports that rank's status and
+    frame, rank 0 gets the frames before it (the failing rank's partial
+    output) and nothing of the ranks after it (src/main.rs:43-53)."""
+    world = 3
+    payloads = [b"frames of rank 0|", b"rank 1 before its failure|", b"rank 2 frames, after the failure"]
+    statuses = [(0, -1), (-42, 17), (0, -1)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_fail, args=(r, world, port, payloads, statuses, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, gst, gfirst, n, out = q.get(timeout=120)
+        got[r] = (gst, gfirst, n, out)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert got[r][:2] == (-42, 17)
+    assert got[2][2] == 0
+    assert got[0][3] == payloads[0] + payloads[1]
+
+
 @pytest.mark.gpu
 def test_decode_sharded_single_rank_gpu():
     from corpus import gen
@@ -100,3 +169,71 @@ def test_decode_sharded_single_rank_gpu():
     st, local, n, gathered = shard.decode_sharded(data, 0, 1, torch.device("cuda", 0))
     assert st == 0 and n == len(src)
     assert bytes(gathered.cpu().numpy().tobytes()) == src
+
+
+def test_bench_strong_shards_cover_the_corpus():
+    """bench.py's strong-scaling split (one corpus, contiguous frame ranges of
+    the replicated frame set): the ranks' compressed bytes and expected
+    outputs concatenate to the whole corpus and its source."""
+    import bench
+    from corpus import gen
+    from zstd_decompressor.batch import frames_index
+    src = gen.text(1 << 20, seed=17)
+    frame_set = gen.frames(src, 100_000, 3)
+    frames = frames_index(frame_set)[0]
+    reps = 3
+    n = len(frames) * reps
+    for world in (1, 2, 5, 8):
+        ranges = shard.partition([frames[k % len(frames)]["src_size"] for k in range(n)], world)
+        parts = [bench.shard_bytes(frame_set, frames, src, reps, b, e) for b, e in ranges]
+        assert b"".join(p[0] for p in parts) == frame_set * reps
+        assert b"".join(p[1] for p in parts) == src * reps
+    assert bench.host_cores()[0] >= 1
+
+
+def _comm_world1_worker(port, q):
+    import torch.distributed as dist
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        import ctypes as C
+        from zstd_decompressor import _lib
+        comm = shard.Comm(0, 1, dev)
+        payload = torch.arange(0, 1 << 20, dtype=torch.int64, device=dev).to(torch.uint8)
+        root = torch.zeros((1 << 20) + 64, dtype=torch.uint8, device=dev)
+        st, res = comm.gather(payload.data_ptr(), 1 << 20, 0, -1, root.data_ptr(), root.numel(),
+                              torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        ok1 = st == 0 and res.status == 0 and res.total_len == 1 << 20 and bool(torch.equal(root[:1 << 20], payload))
+        # the whole sharded decode through the C ABI, on the reference's sample
+        data = open(os.path.join(os.path.dirname(__file__), "golden", "resources", "moby-dick.txt.zst"), "rb").read()
+        expect = oracle.decompress(data)
+        out = torch.zeros(len(expect) + 64, dtype=torch.uint8, device=dev)
+        res2 = _lib.GatherResult()
+        p, n, keep = _lib.buf(data)
+        st2 = _lib.lib().zd_decode_sharded(comm._h, p, n, 0, C.c_void_p(out.data_ptr()), out.numel(), C.byref(res2),
+                                           C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        ok2 = st2 == 0 and res2.status == 0 and res2.total_len == len(expect) and \
+            bytes(out[:len(expect)].cpu().numpy().tobytes()) == expect
+        comm.close()
+        q.put((ok1, ok2))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_comm_gather_and_sharded_decode_world1_gpu():
+    """libzd's RCCL communicator (zd_comm_create / zd_comm_gather) and the
+    one-call zd_decode_sharded, on one GPU (world 1: the RCCL calls run, the
+    sends are to self).  The N>1 legs run in the driver's multi-GPU bench."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_comm_world1_worker, args=(_free_port(), q))
+    p.start()
+    got = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert got == (True, True)

@@ -108,7 +108,11 @@ ZD_HD inline uint32_t k3f_entry(uint32_t e, int k, int al) {
 // order with concrete values.
 // ---------------------------------------------------------------------------
 constexpr uint32_t DIRECT_GIANT = (1u << 29) - 1;
-constexpr uint64_t MAX_FRAME_OUT = 1ull << 27;   // frames with sequences the GPU path decodes
+// Output bounds per executor: the streaming K4 keeps int32 frame positions,
+// K4J u32 ones; a frame with sequences above both is outside the GPU path's
+// domain (ZD_E_OUT_OF_DOMAIN; the reference's own limit is the 8 MiB window).
+constexpr uint64_t K4_MAX_FRAME_OUT = 0x7FFF0000ull;
+constexpr uint64_t K4J_MAX_FRAME_OUT = 0xFFFF0000ull;
 constexpr uint64_t OFF_HUGE = ~0ull >> 1;        // a giant offset (never <= a decoded length)
 
 ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t ofv) {
@@ -179,6 +183,32 @@ ZD_HD inline uint32_t rc_apply(uint32_t b, const uint32_t a[3]) {
 ZD_HD inline void rc_compose(const uint32_t a[3], uint32_t b[3]) {
   const uint32_t c0 = rc_apply(b[0], a), c1 = rc_apply(b[1], a), c2 = rc_apply(b[2], a);
   b[0] = c0; b[1] = c1; b[2] = c2;
+}
+
+// 64-bit repeat-offset codes for K4J's per-block maps (the K4F codes above
+// cap offsets at 2^28; K4J frames go to 4 GiB).  Concrete offsets are below
+// 2^33 (offset_value < 2^32, decrements), so these stay exact:
+//   v < J_SYM                concrete v; J_UNDER = a value after a usize
+//                            underflow (the sequence that underflowed reports
+//                            ZD_E_REF_PANIC; what follows in the frame is moot)
+//   J_SYM | j << 48 | d      incoming rep[j] - d
+constexpr uint64_t J_SYM = 1ull << 63;
+constexpr uint64_t J_UNDER = 1ull << 62;
+constexpr uint64_t J_DMASK = (1ull << 48) - 1;
+ZD_HD inline uint64_t jr_sym(uint32_t j) { return J_SYM | ((uint64_t)j << 48); }
+ZD_HD inline uint64_t jr_dec1(uint64_t v) {
+  if (v >= J_SYM) return v + 1;
+  return (v == 0 || v >= J_UNDER) ? J_UNDER : v - 1;
+}
+// code b evaluated on the incoming slots a[3] (codes or concrete)
+ZD_HD inline uint64_t jr_apply(uint64_t b, const uint64_t a[3]) {
+  if (b < J_SYM) return b;
+  const uint32_t j = (uint32_t)((b >> 48) & 3);
+  const uint64_t d = b & J_DMASK;
+  const uint64_t x = j == 0 ? a[0] : (j == 1 ? a[1] : a[2]);
+  if (x >= J_SYM) return x + d;
+  if (x >= J_UNDER) return J_UNDER;
+  return x >= d ? x - d : J_UNDER;
 }
 
 // ---------------------------------------------------------------------------
@@ -308,7 +338,7 @@ struct FrameDesc {
   uint64_t out_len0;       // bytes already produced before this launch (context API)
   uint32_t first_block;    // into BlockRec[]
   uint32_t nblocks;        // blocks to execute (0 for frames skipped by parse errors)
-  uint32_t lds;            // 1: executed by K4F (whole frame in LDS), 0: by the streaming K4
+  uint32_t lds;            // 1: executed by K4F (whole frame in LDS), 2: by K4J (block-parallel), 0: by the streaming K4
   uint32_t skip;           // leading raw/RLE blocks copied by K0 (the streaming K4 starts after them)
   uint64_t skip_bytes;     // their output bytes
 };
@@ -329,12 +359,47 @@ struct FrameState {
   uint64_t rep[3];         // repeat offsets in/out (decoding_context.rs:20)
 };
 
+// ---------------------------------------------------------------------------
+// K4J: frames of many blocks executed block-parallel (zd_kernels.hip K4J).
+// A frame is laid out as per-byte state in three arrays of its own region
+// [base, base + cap): fin (u8: 0 = final from the scatter, r = made final in
+// pointer-jumping round r, J_PENDING = a match byte still to resolve) and two
+// u32 pointer arrays (the frame position each pending byte copies from), used
+// alternately by the rounds.
+// ---------------------------------------------------------------------------
+constexpr uint8_t J_PENDING = 255;
+constexpr int J_MAX_ROUNDS = 40;
+struct JFrame {
+  uint64_t base;           // byte index of the frame's region in fin / the pointer arrays
+  uint64_t cap;            // bytes of the region (>= the frame's capacity)
+  uint64_t piece0;         // first 16-byte piece of the frame in the rounds' piece numbering
+  uint32_t frame;          // plan frame index
+  uint32_t jb0, njb;       // its blocks: JBlkDesc / JBlk [jb0, jb0 + njb)
+  uint32_t pad;
+};
+struct JBlkDesc {          // static, from the host
+  uint32_t block;          // BlockRec index
+  uint32_t jframe;         // JFrame index
+  uint32_t j;              // block index inside the frame
+  uint32_t pad;
+};
+struct JBlk {              // device: K4J pass results per block
+  uint64_t out_start;      // frame position of the block's first output byte
+  uint64_t size;           // output bytes (literals + match lengths)
+  uint64_t rep_in[3];      // repeat offsets before the block (concrete)
+  uint64_t map[3];         // the block's repeat-offset map (zd_kernels.hip j_rep codes)
+  uint32_t dead;           // 1: not executed (a failure before it, or past the capacity)
+  uint32_t pad;
+};
+
 // Workspace carve-up, all offsets in bytes from the workspace base.
 struct Workspace {
-  uint64_t comp, comp_state, blocks, frames, frame_state;
+  uint64_t comp, comp_state, blocks, frames, frame_state, frame_state0;
   uint64_t list_tables, list_huf, list_seq, list_k4f;   // u32 work lists
   uint64_t copies;                                      // CopyDesc[] for K0
   uint64_t lits, seqs, luts, fses;
+  uint64_t jframes, jblkd, jblk, jpend;                 // K4J descriptors / state / round counters
+  uint64_t jfin, jptr0, jptr1;                          // K4J per-byte arrays
   uint64_t total;
 };
 

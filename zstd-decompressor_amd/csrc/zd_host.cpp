@@ -317,6 +317,10 @@ struct zd_plan {
   std::vector<FrameState> fstate0;
   std::vector<uint32_t> list_tables, list_huf, list_seq, list_k4f;
   std::vector<CopyDesc> copies;         // K0 pieces
+  std::vector<JFrame> jframes;          // K4J frames and their blocks
+  std::vector<JBlkDesc> jblkd;
+  uint64_t j_bytes = 0, j_pieces = 0;
+  uint32_t j_rounds = 0;
   std::vector<uint64_t> frame_cap_off;   // output offset per frame (capacity layout)
   zd_plan_info info{};
   Workspace W{};
@@ -347,6 +351,14 @@ uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 // pays for up to three rounds (scripts/exp_thresholds.sh: 8192 frames 12.1
 // vs 7.7 ms per step)
 constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 3 * 256;
+// K4J (block-parallel execute, pointer jumping) takes the frames of at least
+// K4J_MIN_BLOCKS compressed blocks: the streaming K4 runs a frame's blocks one
+// after another on one wave, which a frame of many blocks cannot hide behind
+// other frames unless the plan holds thousands of them
+// (K4J_MAX_FRAMES).  ZD_K4J=1 / 0 forces it on (every frame with a
+// compressed block) / off.
+constexpr uint32_t K4J_MIN_BLOCKS = 16;
+constexpr size_t K4J_MAX_FRAMES = 1024;
 constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
 
 // Builds device-side descriptors from the host frames.  `prev_*` seed the
@@ -357,10 +369,23 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   uint32_t lut_slots = 0, fse_slots = 0;
   bool exact = true;
   P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
-  P->frame_cap_off.clear();
+  P->frame_cap_off.clear(); P->jframes.clear(); P->jblkd.clear();
   static const char* k4f_env = getenv("ZD_K4F");
   const bool k4f_on = k4f_env ? atoi(k4f_env) == 1
                               : P->frames.size() >= K4F_AUTO_MIN_FRAMES && P->frames.size() <= K4F_AUTO_MAX_FRAMES;
+  static const char* k4j_env = getenv("ZD_K4J");
+  const int k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0
+                       : (k4j_env ? atoi(k4j_env) : -1);
+  auto ncomp_of = [](const HostFrame& hf) {
+    uint32_t c = 0;
+    for (const HostBlock& hb : hf.blocks) c += hb.type == 2;
+    return c;
+  };
+  size_t j_candidates = 0;
+  if (k4j_mode < 0 && out_len0 == 0)
+    for (const HostFrame& hf : P->frames) j_candidates += hf.key == KEY_NONE && ncomp_of(hf) >= K4J_MIN_BLOCKS;
+  const bool k4j_auto = j_candidates > 0 && j_candidates <= K4J_MAX_FRAMES;
+  uint64_t j_base = 0, j_pieces = 0, j_maxseq = 0;
   for (size_t fi = 0; fi < P->frames.size(); fi++) {
     HostFrame& hf = P->frames[fi];
     FrameDesc fd{};
@@ -458,18 +483,48 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     }
     if (frame_failed_host) fd.nblocks = 0;
     if (fixed_cap) cap = fixed_cap;
-    // offset codes stay exact below 2^28 (zd_common.h); larger frames with
-    // sequences are outside the GPU path's domain
-    if (cap > MAX_FRAME_OUT && seqs_in_frame)
-      fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
     fd.out = out_off;
     fd.out_cap = cap;
+    // K4J: frames of many compressed blocks (u32 positions)
+    const uint32_t ncomp = ncomp_of(hf);
+    const bool to_j = out_len0 == 0 && !frame_failed_host && fd.nblocks && ncomp && hf.d.kind == ZD_FRAME_ZSTD &&
+                      cap <= K4J_MAX_FRAME_OUT && (k4j_mode >= 0 ? k4j_mode == 1 : (k4j_auto && ncomp >= K4J_MIN_BLOCKS));
+    // the streaming K4 keeps int32 frame positions: larger frames with
+    // sequences that K4J does not take are outside the GPU path's domain
+    if (!to_j && cap > K4_MAX_FRAME_OUT && seqs_in_frame)
+      fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
+    if (to_j) {
+      fd.lds = 2;
+      JFrame jf{};
+      // the region's byte index has the output offset's alignment mod 16, so
+      // 16-byte pieces of the output, fin and the pointer arrays line up
+      jf.base = align_up(j_base, 16) + (out_off & 15);
+      jf.cap = cap;
+      jf.piece0 = j_pieces;
+      jf.frame = (uint32_t)fi;
+      jf.jb0 = (uint32_t)P->jblkd.size();
+      jf.njb = fd.nblocks;
+      uint64_t nseq = 0;
+      for (uint32_t k = 0; k < fd.nblocks; k++) {
+        JBlkDesc d{};
+        d.block = fd.first_block + k;
+        d.jframe = (uint32_t)P->jframes.size();
+        d.j = k;
+        P->jblkd.push_back(d);
+        const BlockRec& br = P->blocks[fd.first_block + k];
+        if (br.comp >= 0) nseq += P->comps[(size_t)br.comp].nseq;
+      }
+      j_maxseq = std::max(j_maxseq, nseq);
+      j_base = jf.base + cap + 16;
+      j_pieces += (cap + 15) / 16;
+      P->jframes.push_back(jf);
+    }
     // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
     // executes the frames that fit it in plans of 256-768 frames, where the
     // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
     // it is slower on C4.  ZD_K4F=1 / 0 forces it on / off.
-    fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
-    if (fd.lds) P->list_k4f.push_back((uint32_t)fi);
+    if (!to_j) fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
+    if (fd.lds == 1) P->list_k4f.push_back((uint32_t)fi);
     // Leading raw / RLE blocks (skippable payloads too) have output offsets
     // known here: K0 copies them in parallel pieces, the streaming K4 starts
     // after them (a frame of raw/RLE blocks only never reaches K4's loop).
@@ -507,6 +562,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.blocks = carve(sizeof(BlockRec) * std::max<size_t>(P->blocks.size(), 1));
   W.frames = carve(sizeof(FrameDesc) * std::max<size_t>(P->fdesc.size(), 1));
   W.frame_state = carve(sizeof(FrameState) * std::max<size_t>(P->fdesc.size(), 1));
+  W.frame_state0 = carve(sizeof(FrameState) * std::max<size_t>(P->fdesc.size(), 1));
   W.list_tables = carve(4 * std::max<size_t>(P->list_tables.size(), 1));
   W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
   W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
@@ -516,6 +572,24 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.seqs = carve(8 * nrec + 64);
   W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
   W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint32_t>(fse_slots, 1));
+  // K4J: pointer jumping resolves every match byte within ceil(log2(matches
+  // + 1)) rounds (each pointer chain ends at a literal after at most one hop
+  // per earlier match; each round halves the hops left)
+  P->j_bytes = P->jframes.empty() ? 0 : j_base + 16;
+  P->j_pieces = j_pieces;
+  P->j_rounds = 0;
+  if (!P->jframes.empty()) {
+    uint32_t r = 1;
+    while (r < (uint32_t)J_MAX_ROUNDS - 1 && (1ull << r) <= j_maxseq + 1) r++;
+    P->j_rounds = r + 1;
+  }
+  W.jframes = carve(sizeof(JFrame) * std::max<size_t>(P->jframes.size(), 1));
+  W.jblkd = carve(sizeof(JBlkDesc) * std::max<size_t>(P->jblkd.size(), 1));
+  W.jblk = carve(sizeof(JBlk) * std::max<size_t>(P->jblkd.size(), 1));
+  W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
+  W.jfin = carve(P->j_bytes + 64);
+  W.jptr0 = carve(4 * P->j_bytes + 64);
+  W.jptr1 = carve(4 * P->j_bytes + 64);
   W.total = o;
 
   zd_plan_info& I = P->info;
@@ -551,6 +625,9 @@ int upload_plan(zd_plan* P) {
   if (int r = up(P->W.list_seq, P->list_seq.data(), P->list_seq.size() * 4)) return r;
   if (int r = up(P->W.list_k4f, P->list_k4f.data(), P->list_k4f.size() * 4)) return r;
   if (int r = up(P->W.copies, P->copies.data(), P->copies.size() * sizeof(CopyDesc))) return r;
+  if (int r = up(P->W.frame_state0, P->fstate0.data(), P->fstate0.size() * sizeof(FrameState))) return r;
+  if (int r = up(P->W.jframes, P->jframes.data(), P->jframes.size() * sizeof(JFrame))) return r;
+  if (int r = up(P->W.jblkd, P->jblkd.data(), P->jblkd.size() * sizeof(JBlkDesc))) return r;
   if (!P->info.out_exact) {
     P->staging_bytes = P->info.out_bytes;
     HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
@@ -701,6 +778,7 @@ const char* zd_status_name(int s) {
     case ZD_E_HIP: return "HipError";
     case ZD_E_NO_MEMORY: return "NoMemory";
     case ZD_E_NOT_DECODED: return "NotDecoded";
+    case ZD_E_COMM: return "CommError";
     default: return "Unknown";
   }
 }
@@ -755,6 +833,12 @@ int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) 
             std::chrono::duration<double, std::milli>(ti - t0).count(),
             std::chrono::duration<double, std::milli>(t1 - ti).count());
   int r = upload_plan(P);
+  // the second stream and its events (K2 beside K3, opt-in overlap) exist
+  // from here on, so zd_decode_async creates nothing
+  if (!r && (hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking) != hipSuccess ||
+             hipEventCreateWithFlags(&P->fork, hipEventDisableTiming) != hipSuccess ||
+             hipEventCreateWithFlags(&P->join, hipEventDisableTiming) != hipSuccess))
+    r = ZD_E_HIP;
   if (r) { zd_plan_destroy(P); return r; }
   const auto t2 = std::chrono::steady_clock::now();
   P->info.host_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
@@ -806,12 +890,17 @@ int zd_plan_kernel_times(zd_plan* P, const char** names, float* ms, int cap, int
 
 int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst_cap, void* stream) {
   if (!P) return ZD_E_INVALID_ARG;
-  if (P->info.out_exact && dst_cap < P->info.out_bytes) return ZD_E_DST_TOO_SMALL;
+  // out_bytes bounds the output in both layouts (the staging layout is
+  // compacted into d_dst by zd_plan_results)
+  if (dst_cap < P->info.out_bytes) return ZD_E_DST_TOO_SMALL;
   hipStream_t s = (hipStream_t)stream;
-  // frame and block states are reset every launch (keys, lengths, repeat offsets, flags)
-  HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->fstate0.data(), P->fstate0.size() * sizeof(FrameState),
-                        hipMemcpyHostToDevice, s));
+  // frame and block states are reset every launch (keys, lengths, repeat
+  // offsets, flags) from device-resident copies: no host memory is read, so
+  // a graph captured around this call replays the reset
+  HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->d_ws + P->W.frame_state0,
+                        P->fstate0.size() * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
+  if (!P->jframes.empty()) HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
   LaunchArgs a{};
   a.src = d_src;
   a.src_size = P->info.src_bytes;
@@ -824,6 +913,10 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_frames = (uint32_t)P->fdesc.size();
   a.n_k4f = (uint32_t)P->list_k4f.size();
   a.n_copies = (uint32_t)P->copies.size();
+  a.n_jframes = (uint32_t)P->jframes.size();
+  a.n_jblk = (uint32_t)P->jblkd.size();
+  a.j_rounds = P->j_rounds;
+  a.j_pieces = P->j_pieces;
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
@@ -846,12 +939,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
     while (k < P->list_seq.size() && P->comps[P->list_seq[k]].frame < a.n_frames_a) k++;
     a.n_seq_a = k;
   }
-  if (!P->aux && (fork || a.overlap)) {
-    HIPCHK(hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&P->fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&P->join, hipEventDisableTiming));
-  }
-  a.aux = P->aux; a.fork = P->fork; a.join = P->join;
+  if (fork || a.overlap) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
   if (const char* g = getenv("ZD_K4_GRID")) a.k4_grid = (uint32_t)strtoul(g, nullptr, 0);
   HIPCHK(launch_pipeline(a));
   P->launched = true;
@@ -1177,7 +1265,9 @@ int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consume
     // chained them through the virtual block's own FSE/Compressed modes)
     P.blocks[0].type = 5;    // skip in execute
     FrameState& fs = P.fstate0[0];
-    fs.key = KEY_NONE;
+    // build_plan's keys came from the virtual block; keep only a capacity
+    // limit (PH_LIMIT: the context past the streaming K4's int32 positions)
+    if (fs.key != KEY_NONE && key_phase(fs.key) != PH_LIMIT) fs.key = KEY_NONE;
     // re-derive host decode errors for the real block only
     CompBlock& cb = P.comps[1];
     if (cb.lit_type == LIT_TREELESS && !c->has_huf)

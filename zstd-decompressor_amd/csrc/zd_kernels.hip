@@ -23,7 +23,7 @@
 namespace zd {
 
 const char* const kKernelNames[N_KERNELS] = {"zd_k_rawcopy", "zd_k_tables", "zd_k_huffman", "zd_k_sequences",
-                                             "zd_k_execute"};
+                                             "zd_k_execute", "zd_k_jexec"};
 
 // ---------------------------------------------------------------------------
 // constants (decoders/sequence.rs:95-191, sequences.rs:29-39)
@@ -2263,6 +2263,543 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 }
 
 // ---------------------------------------------------------------------------
+// K4J: execute of frames of many blocks, block-parallel (decoding_context.rs:
+// 50-106 + block.rs:74-99).  The streaming K4 runs a frame's sequences in
+// order on one wave: a 100 MB frame (the stock `zstd enwik8` shape) is ~11 M
+// sequences one batch after another.  K4J takes the frame's serial
+// dependencies apart:
+//   KJ1 zd_k_jsum     one wave per block: the block's output size (literals +
+//                     match lengths) and its repeat-offset map (decode_offset
+//                     as a function of the three offsets coming in, jr codes)
+//   KJ2 zd_k_jprefix  one wave per frame: scans over the blocks give each
+//                     block's output position and the concrete repeat offsets
+//                     entering it; the capacity check
+//   KJ3 zd_k_jscatter one wave per block: the sequences with concrete offsets
+//                     and the reference's checks; literal bytes are written
+//                     final, every match byte as a pointer to the frame
+//                     position it copies (q - off + j mod off: the period of an
+//                     overlapping match, as the reference's byte-by-byte push)
+//   KJ4 zd_k_jround   pointer jumping over the match bytes: a byte whose
+//                     source is final copies it, else takes over its source's
+//                     pointer, so round r resolves chains of up to 2^r - 1
+//                     hops.  A chain ends at a literal after at most one hop
+//                     per earlier match: ceil(log2(matches + 1)) rounds
+//                     finish (launched with an early exit once nothing is
+//                     pending).
+// Per byte of these frames: fin (u8) and two u32 pointer arrays, used
+// alternately by the rounds (zd_common.h JFrame).
+// ---------------------------------------------------------------------------
+__device__ inline bool j_live(uint64_t key, uint32_t j) {
+  // a parse error ends the frame before any block decodes (frame.rs:198-230);
+  // a decode error (or a capacity limit) at block b leaves blocks < b to run
+  return key == KEY_NONE || (key_phase(key) != PH_PARSE && key_block(key) > j);
+}
+
+__device__ inline uint64_t shfl_up_u64(uint64_t x, int d) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d, 64);
+  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ inline uint64_t wave_scan_u64(uint64_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = shfl_up_u64(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+// wave-inclusive composition of repeat-offset maps, lane order
+__device__ inline void j_scan_map(uint64_t m[3], int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t a[3];
+    a[0] = shfl_up_u64(m[0], d);
+    a[1] = shfl_up_u64(m[1], d);
+    a[2] = shfl_up_u64(m[2], d);
+    if (lane >= d) {
+      const uint64_t c0 = jr_apply(m[0], a), c1 = jr_apply(m[1], a), c2 = jr_apply(m[2], a);
+      m[0] = c0; m[1] = c1; m[2] = c2;
+    }
+  }
+}
+
+// The block's LL/OF/ML symbols (K1's sym entries) -> LDS.
+__device__ inline void j_stab(uint8_t (*stab)[FSE_TAB], const CompBlock& C, const CompBlock* __restrict__ comp,
+                              const CompState* __restrict__ cstate, const uint16_t* __restrict__ fses, int lane) {
+  for (int k = 0; k < 3; k++) {
+    const uint32_t s = (uint32_t)C.tab_src[k];
+    const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+    const int cnt = 1 << cstate[s].al[k];
+    for (int e = lane; e < cnt; e += 64) stab[k][e] = (uint8_t)(g[e] & 63);
+  }
+  k4_sync();
+}
+
+// update_symbol_value (decoders/sequence.rs:41-55) from a K3 record: OF, ML,
+// LL extra bits below the recorded position, in that order.
+__device__ inline void j_values(uint64_t rec, const WinU& w, const uint8_t (*stab)[FSE_TAB], uint32_t& ll,
+                                uint32_t& ml, uint32_t& ofv) {
+  const uint32_t stt = (uint32_t)(rec >> 32);
+  const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
+  uint32_t llbase, llb, mlbase, mlb;
+  ll_code(llc, &llbase, &llb);
+  ml_code(mlc, &mlbase, &mlb);
+  uint64_t t = winu_top(w, 0);
+  const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
+  ofv = (1u << ofc) + ob;
+  ml = mlbase + mb;
+  ll = llbase + lb;
+}
+
+// decode_offset (decoding_context.rs:50-75) over lanes [0, k) of a batch, in
+// order: fresh offsets (offset_value > 3) push their value, the rare repeat
+// codes are walked on the scalar unit.  SYM: the state holds jr codes (KJ1's
+// maps; no errors: a null offset leaves the state, and the block that holds
+// it reports it in KJ3), else concrete values with the reference's errors
+// (*bad_lane = the first failing lane, -1 if none).  Returns each lane's
+// offset; rep[] becomes the state after lane k - 1.
+template <bool SYM>
+__device__ inline uint64_t j_offsets(uint32_t ofv, uint32_t ll, int k, uint64_t rep[3], int* bad_lane, int* bad_code) {
+  const int lane = threadIdx.x & 63;
+  const bool fresh = ofv > 3;
+  const uint64_t val = (uint64_t)ofv - 3;
+  uint64_t off = val;
+  uint64_t rm = __ballot(lane < k && !fresh);
+  uint64_t r0 = rep[0], r1 = rep[1], r2 = rep[2];
+  int prev = -1;
+  *bad_lane = -1;
+  *bad_code = 0;
+  while (rm) {
+    const int ri = __ffsll((long long)rm) - 1;
+    rm &= rm - 1;
+    uint64_t a0, a1, a2;
+    rep_push(val, ri - prev - 1, ri, r0, r1, r2, &a0, &a1, &a2);
+    const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)ofv, ri);
+    const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)ll, ri);
+    uint64_t o = a0;
+    int e = 0;
+    if (oi == 0) {
+      e = SYM ? 0 : ZD_E_NULL_OFFSET;
+    } else {
+      const uint32_t idx = oi - (li != 0 ? 1u : 0u);
+      if (idx == 0) { o = a0; }
+      else if (idx == 1) { o = a1; a1 = a0; a0 = o; }
+      else if (idx == 2) { o = a2; a2 = a1; a1 = a0; a0 = o; }
+      else if (!SYM && a0 == 0) { e = ZD_E_REF_PANIC; }     // usize underflow of offsets[0] -= 1
+      else { o = SYM ? jr_dec1(a0) : a0 - 1; a2 = a1; a1 = a0; a0 = o; }
+    }
+    if (lane == ri) off = o;
+    r0 = a0; r1 = a1; r2 = a2;
+    prev = ri;
+    if (e) {
+      *bad_lane = ri;
+      *bad_code = e;
+      return off;
+    }
+  }
+  rep_push(val, k - 1 - prev, k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
+  return off;
+}
+
+__device__ inline uint64_t wave_sum_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, d, 64);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), d, 64);
+    x += ((uint64_t)hi << 32) | lo;
+  }
+  return x;
+}
+
+// Software pipeline over a block's records shared by KJ1 and KJ3: records two
+// batches ahead, bitstream windows one ahead (K4's order).
+struct JRecs {
+  const uint64_t* SQ;
+  const uint8_t* bsp;
+  uintptr_t base;
+  uint32_t n;
+  uint64_t recA, recB;
+  WinU winA;
+  __device__ inline uint64_t at(uint32_t i) const { return i < n ? SQ[i] : 0; }
+  __device__ inline WinU win(uint64_t r, bool v) const { return winu_load(bsp, base, v ? (int32_t)(uint32_t)r : 0); }
+  __device__ inline void start(uint32_t s0, int lane) {
+    recA = at(s0 + lane);
+    recB = at(s0 + 64 + lane);
+    winA = win(recA, s0 + lane < n);
+  }
+  // this batch's (rec, window) in recA / winA; issues the next loads
+  __device__ inline void next(uint32_t s0, int lane) {
+    const WinU wb = win(recB, s0 + 64 + lane < n);
+    const uint64_t rc = at(s0 + 128 + lane);
+    recA = recB; winA = wb; recB = rc;
+  }
+};
+
+__global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src, const FrameState* __restrict__ fstate,
+                                                const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp,
+                                                const CompState* __restrict__ cstate, const uint64_t* __restrict__ seqs,
+                                                const uint16_t* __restrict__ fses, const JFrame* __restrict__ jframes,
+                                                const JBlkDesc* __restrict__ jd, JBlk* __restrict__ jb) {
+  __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
+  const int lane = threadIdx.x;
+  const uint32_t e = blockIdx.x;
+  const JBlkDesc D = jd[e];
+  const uint64_t key0 = fstate[jframes[D.jframe].frame].key;
+  const BlockRec B = blocks[D.block];
+  uint64_t rep[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
+  uint64_t size = 0;
+  uint32_t dead = j_live(key0, D.j) ? 0u : 1u;
+  if (!dead && B.type != 2) {
+    size = B.size;                                  // raw / RLE (block.rs:76-79)
+  } else if (!dead) {
+    const CompState CS = cstate[B.comp];
+    const CompBlock C = comp[B.comp];
+    if (CS.stop) {
+      dead = 1;
+    } else {
+      const uint32_t nl = (C.lit_type == LIT_RAW || C.lit_type == LIT_RLE) ? C.lit_regen : CS.lit_count;
+      uint64_t summ = 0;
+      const uint32_t n = C.nseq;
+      if (n) {
+        j_stab(stab, C, comp, cstate, fses, lane);
+        JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n};
+        R.start(0, lane);
+        for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+          const int k = (int)min(64u, n - s0);
+          uint32_t ll = 0, ml = 0, ofv = 4;
+          if (lane < k) j_values(R.recA, R.winA, stab, ll, ml, ofv);
+          R.next(s0, lane);
+          summ += ml;
+          int bl, bc;
+          (void)j_offsets<true>(ofv, ll, k, rep, &bl, &bc);
+        }
+      }
+      size = nl + wave_sum_u64(summ);
+    }
+  }
+  if (lane == 0) {
+    jb[e].size = size;
+    jb[e].map[0] = rep[0];
+    jb[e].map[1] = rep[1];
+    jb[e].map[2] = rep[2];
+    jb[e].dead = dead;
+  }
+}
+
+__global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__ frames, FrameState* fstate,
+                                                   const JFrame* __restrict__ jframes, const JBlkDesc* __restrict__ jd,
+                                                   JBlk* jb) {
+  const int lane = threadIdx.x;
+  const JFrame JF = jframes[blockIdx.x];
+  const uint64_t cap = frames[JF.frame].out_cap;
+  FrameState* S = &fstate[JF.frame];
+  uint64_t pos = 0;
+  uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
+  bool stop = false;
+  for (uint32_t c = 0; c < JF.njb; c += 64) {
+    const uint32_t e = JF.jb0 + c + lane;
+    const bool v = c + lane < JF.njb;
+    uint64_t size = 0, m[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
+    uint32_t dead = 1;
+    if (v && !stop) {
+      size = jb[e].size;
+      m[0] = jb[e].map[0]; m[1] = jb[e].map[1]; m[2] = jb[e].map[2];
+      dead = jb[e].dead;
+    }
+    // blocks from the first dead one on do not run
+    const uint64_t dm = __ballot(v && dead);
+    const int fd = dm ? __ffsll((long long)dm) - 1 : 64;
+    bool live = v && !stop && lane < fd;
+    if (!live) { size = 0; m[0] = jr_sym(0); m[1] = jr_sym(1); m[2] = jr_sym(2); }
+    uint64_t incl = wave_scan_u64(size, lane);
+    // past the frame's capacity (its Frame_Content_Size; the reference checks
+    // none): out of the GPU path's domain from that block on
+    const uint64_t om = __ballot(live && pos + incl > cap);
+    if (om) {
+      const int fo = __ffsll((long long)om) - 1;
+      if (lane == fo) key_min(fstate, JF.frame, make_key(PH_LIMIT, jd[e].j, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
+      if (lane >= fo) { live = false; size = 0; m[0] = jr_sym(0); m[1] = jr_sym(1); m[2] = jr_sym(2); }
+      incl = wave_scan_u64(size, lane);
+    }
+    j_scan_map(m, lane);
+    uint64_t ex[3] = {shfl_up_u64(m[0], 1), shfl_up_u64(m[1], 1), shfl_up_u64(m[2], 1)};
+    if (lane == 0) { ex[0] = jr_sym(0); ex[1] = jr_sym(1); ex[2] = jr_sym(2); }
+    if (v) {
+      jb[e].out_start = pos + incl - size;
+      jb[e].rep_in[0] = jr_apply(ex[0], rep);
+      jb[e].rep_in[1] = jr_apply(ex[1], rep);
+      jb[e].rep_in[2] = jr_apply(ex[2], rep);
+      jb[e].dead = live ? 0u : 1u;
+    }
+    // dead lanes hold identity maps and no bytes: lane 63 composes the live ones
+    const uint64_t mt[3] = {readlane_u64(m[0], 63), readlane_u64(m[1], 63), readlane_u64(m[2], 63)};
+    const uint64_t nr0 = jr_apply(mt[0], rep), nr1 = jr_apply(mt[1], rep), nr2 = jr_apply(mt[2], rep);
+    rep[0] = nr0; rep[1] = nr1; rep[2] = nr2;
+    pos += readlane_u64(incl, 63);
+    if (fd < 64 || om) stop = true;
+  }
+  if (lane == 0) {
+    S->out_len = pos;
+    S->rep[0] = rep[0];
+    S->rep[1] = rep[1];
+    S->rep[2] = rep[2];
+  }
+}
+
+typedef __attribute__((address_space(1))) u32x4a1 g_u32x4a1;
+// Bytes [x0, x1) of a 16-byte piece (x1 - x0 <= 16, b = byte index in the
+// piece) go to p + x0: one 16-byte store for a whole piece, else byte by byte
+// (a partial piece shares its aligned 16 bytes with another lane's).
+__device__ inline void j_store16(uint8_t* p, const u32x4& v, uint32_t n) {
+  if (n == 16) { *(g_u32x4a1*)p = v; return; }
+#pragma unroll
+  for (uint32_t b = 0; b < 16; b++)
+    if (b < n) p[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
+}
+
+// n literal bytes from s (HBM) or the fill byte at frame position P0: final.
+__device__ void j_fill_lits(uint8_t* out, uint8_t* fin, uint32_t P0, uint32_t n, const uint8_t* s, uint32_t fill,
+                            int lane) {
+  if (!n) return;
+  const uint32_t g = (uint32_t)((16 - ((uintptr_t)(out + P0) & 15)) & 15);
+  const uint32_t np = n > g ? 1 + (n - g + 15) / 16 : 1;
+  const u32x4 f4 = (u32x4){fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u};
+  const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
+  for (uint32_t pi = lane; pi < np; pi += 64) {
+    const uint32_t x0 = pi == 0 ? 0 : g + 16 * (pi - 1);
+    const uint32_t x1 = pi == 0 ? min(g, n) : min(n, g + 16 * pi);
+    if (x0 >= x1) continue;
+    u32x4 v = f4;
+    if (s) {
+      if (x1 - x0 == 16) {
+        v = ldg16(s + x0);
+      } else {
+        v = z4;
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++)
+          if (x0 + b < x1) v[b >> 2] |= (uint32_t)s[x0 + b] << (8 * (b & 3));
+      }
+    }
+    j_store16(out + P0 + x0, v, x1 - x0);
+    j_store16(fin + P0 + x0, z4, x1 - x0);
+  }
+}
+
+__global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ src, uint8_t* outbase,
+                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
+                                                    const BlockRec* __restrict__ blocks,
+                                                    const CompBlock* __restrict__ comp,
+                                                    const CompState* __restrict__ cstate,
+                                                    const uint8_t* __restrict__ lits, const uint64_t* __restrict__ seqs,
+                                                    const uint16_t* __restrict__ fses,
+                                                    const JFrame* __restrict__ jframes,
+                                                    const JBlkDesc* __restrict__ jd, const JBlk* __restrict__ jb,
+                                                    uint8_t* jfin, uint32_t* jptr) {
+  __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
+  __shared__ uint32_t sa[65], sll[64], soff[64], slp[64];
+  const int lane = threadIdx.x;
+  const uint32_t e = blockIdx.x;
+  if (jb[e].dead) return;
+  const JBlkDesc D = jd[e];
+  const JFrame JF = jframes[D.jframe];
+  const FrameDesc F = frames[JF.frame];
+  uint8_t* out = outbase + F.out;
+  uint8_t* fin = jfin + JF.base;
+  uint32_t* ptr = jptr + JF.base;
+  const BlockRec B = blocks[D.block];
+  uint32_t pos = (uint32_t)jb[e].out_start;
+  if (B.type != 2) {
+    j_fill_lits(out, fin, pos, B.size, B.type == 1 ? nullptr : src + B.src, B.rle, lane);
+    return;
+  }
+  const CompBlock C = comp[B.comp];
+  const CompState CS = cstate[B.comp];
+  const uint8_t* lsrc = nullptr;
+  uint32_t lfill = 0, nl;
+  if (C.lit_type == LIT_RAW) { lsrc = src + C.src + C.lit_data; nl = C.lit_regen; }
+  else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle; nl = C.lit_regen; }
+  else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
+  uint32_t lit_cursor = 0;
+  const uint32_t n = C.nseq;
+  if (n) {
+    uint64_t rep[3] = {jb[e].rep_in[0], jb[e].rep_in[1], jb[e].rep_in[2]};
+    j_stab(stab, C, comp, cstate, fses, lane);
+    JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n};
+    R.start(0, lane);
+    for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+      const int k = (int)min(64u, n - s0);
+      const bool valid = lane < k;
+      uint32_t ll = 0, ml = 0, ofv = 4;
+      if (valid) j_values(R.recA, R.winA, stab, ll, ml, ofv);
+      R.next(s0, lane);
+      int bl, bc;
+      const uint64_t off = j_offsets<false>(ofv, ll, k, rep, &bl, &bc);
+      const uint32_t tot = ll + ml;
+      const uint32_t inc_tot = wave_scan_incl(tot), inc_ll = wave_scan_incl(ll);
+      const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
+      // checks (decoding_context.rs:84-90, D9), in sequence order
+      const uint64_t before = (uint64_t)pos + opos;
+      const bool dbad = valid && lane == bl;
+      const bool imp = valid && !dbad && ((uint64_t)lit_cursor + lpos + ll > nl || off > before + ll);
+      const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
+      const uint64_t badm = __ballot(dbad || imp || panic);
+      if (badm) {
+        const int b = __ffsll((long long)badm) - 1;
+        const int code = __shfl(dbad ? bc : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
+        if (lane == 0) key_min(fstate, JF.frame, make_key(PH_DECODE, D.j, DS_EXECUTE, s0 + (uint32_t)b, code));
+        return;
+      }
+      const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, k - 1);
+      const uint32_t Lsum = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, k - 1);
+      if (valid) {
+        sa[lane] = opos;
+        sll[lane] = ll;
+        soff[lane] = (uint32_t)off;
+        slp[lane] = lit_cursor + lpos;
+      }
+      if (lane == 0) sa[k] = T;
+      k4_sync();
+      // the batch's bytes [pos, pos + T) in 16-byte pieces (aligned in the
+      // output): the sequence of each byte by a search of the batch's starts
+      const uint32_t g = (uint32_t)((16 - ((uintptr_t)(out + pos) & 15)) & 15);
+      const uint32_t np = T > g ? 1 + (T - g + 15) / 16 : 1;
+      for (uint32_t pi = lane; pi < np; pi += 64) {
+        const uint32_t x0 = pi == 0 ? 0 : g + 16 * (pi - 1);
+        const uint32_t x1 = pi == 0 ? min(g, T) : min(T, g + 16 * pi);
+        if (x0 >= x1) continue;
+        int i = 0;
+#pragma unroll
+        for (int st = 32; st; st >>= 1)
+          if (i + st < k && sa[i + st] <= x0) i += st;
+        uint32_t a = sa[i], nx = sa[i + 1], l = sll[i], o = soff[i], lp = slp[i];
+        u32x4 vo = (u32x4){0u, 0u, 0u, 0u}, vf = vo;
+        uint32_t pw[16];
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++) {
+          const uint32_t x = x0 + b;
+          pw[b] = 0;
+          if (x < x1) {
+            while (x >= nx) { i++; a = nx; nx = sa[i + 1]; l = sll[i]; o = soff[i]; lp = slp[i]; }
+            const uint32_t rel = x - a;
+            if (rel < l) {
+              const uint32_t byte = lsrc ? lsrc[lp + rel] : lfill;
+              vo[b >> 2] |= byte << (8 * (b & 3));
+            } else {
+              const uint32_t jj = rel - l;
+              pw[b] = pos + a + l - o + (jj < o ? jj : jj % o);
+              vf[b >> 2] |= (uint32_t)J_PENDING << (8 * (b & 3));
+            }
+          }
+        }
+        const uint32_t nb = x1 - x0;
+        j_store16(out + pos + x0, vo, nb);
+        j_store16(fin + pos + x0, vf, nb);
+        uint32_t* pp = ptr + pos + x0;
+        if (nb == 16) {
+#pragma unroll
+          for (int w = 0; w < 4; w++) *(g_u32x4a1*)(pp + 4 * w) = (u32x4){pw[4 * w], pw[4 * w + 1], pw[4 * w + 2], pw[4 * w + 3]};
+        } else {
+#pragma unroll
+          for (uint32_t b = 0; b < 16; b++)
+            if (b < nb) pp[b] = pw[b];
+        }
+      }
+      k4_sync();
+      lit_cursor += Lsum;
+      pos += T;
+    }
+  }
+  // leftover literals (decoding_context.rs:101-103)
+  if (lit_cursor < nl) j_fill_lits(out, fin, pos, nl - lit_cursor, lsrc ? lsrc + lit_cursor : nullptr, lfill, lane);
+}
+
+// One pointer-jumping round over the K4J frames' bytes, 16 per thread.
+// Round r trusts fin values below r (bytes made final by an earlier launch,
+// whose output bytes are visible); a byte made final in this round reads as
+// pending, and its pointer (written by round r - 1) still holds.
+__global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const FrameDesc* __restrict__ frames,
+                                                   FrameState* fstate, const JFrame* __restrict__ jframes,
+                                                   uint32_t n_jframes, uint64_t n_pieces, uint8_t* jfin,
+                                                   const uint32_t* __restrict__ pa, uint32_t* __restrict__ pb,
+                                                   uint32_t* pend, uint32_t r, uint32_t last) {
+  if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
+  uint32_t mine = 0;
+  for (uint64_t pc = (uint64_t)blockIdx.x * 256 + threadIdx.x; pc < n_pieces; pc += (uint64_t)gridDim.x * 256) {
+    uint32_t lo = 0, hi = n_jframes;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (jframes[mid].piece0 <= pc) lo = mid;
+      else hi = mid;
+    }
+    const JFrame JF = jframes[lo];
+    const FrameState* S = &fstate[JF.frame];
+    if (S->key != KEY_NONE) continue;
+    const uint64_t total = S->out_len;
+    const uint64_t p0 = 16 * (pc - JF.piece0);
+    if (p0 >= total) continue;
+    const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
+    uint8_t* fin = jfin + JF.base;
+    u32x4 vf = *(g_u32x4a1*)(fin + p0);
+    uint32_t pm = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b++)
+      pm |= (b < nb && ((vf[b >> 2] >> (8 * (b & 3))) & 255) == J_PENDING) ? (1u << b) : 0u;
+    if (!pm) continue;
+    uint8_t* out = outbase + frames[JF.frame].out;
+    const uint32_t* A = pa + JF.base;
+    uint32_t* Bp = pb + JF.base;
+    uint32_t q[16];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const u32x4 t = *(const g_u32x4a1*)(A + p0 + 4 * w);
+      q[4 * w] = t.x; q[4 * w + 1] = t.y; q[4 * w + 2] = t.z; q[4 * w + 3] = t.w;
+    }
+    u32x4 vo = *(g_u32x4a1*)(out + p0);
+    uint32_t fs[16], os[16], ns[16];
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b++) {
+      fs[b] = 0; os[b] = 0; ns[b] = 0;
+      if ((pm >> b) & 1) {
+        const uint32_t s = q[b] < total ? q[b] : 0;   // (always below p0 + b by construction)
+        fs[b] = fin[s];
+        os[b] = out[s];
+        ns[b] = A[s];
+      }
+    }
+    uint32_t still = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b++) {
+      if ((pm >> b) & 1) {
+        const uint32_t sh = 8 * (b & 3);
+        if (fs[b] < r) {
+          vo[b >> 2] = (vo[b >> 2] & ~(255u << sh)) | (os[b] << sh);
+          vf[b >> 2] = (vf[b >> 2] & ~(255u << sh)) | (r << sh);
+        } else {
+          q[b] = ns[b];
+          still |= 1u << b;
+        }
+      }
+    }
+    j_store16(out + p0, vo, nb);
+    j_store16(fin + p0, vf, nb);
+    if (still) {
+      if (nb == 16) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) *(g_u32x4a1*)(Bp + p0 + 4 * w) = (u32x4){q[4 * w], q[4 * w + 1], q[4 * w + 2], q[4 * w + 3]};
+      } else {
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++)
+          if ((still >> b) & 1) Bp[p0 + b] = q[b];
+      }
+      mine++;
+      if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
+    }
+  }
+  const uint64_t bm = __ballot(mine != 0);
+  if ((threadIdx.x & 63) == 0 && bm) atomicAdd(&pend[r], (uint32_t)__popcll(bm));
+}
+
+// ---------------------------------------------------------------------------
 // K0: raw / RLE blocks at the head of a frame (block.rs:78-79: Raw appends
 // the bytes, RLE the byte `size` times), whose output offsets the planner
 // knows.  One 256-thread workgroup per piece of <= 32 KiB: 16-byte loads,
@@ -2422,6 +2959,28 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses, (const uint32_t*)(ws + W.list_k4f));
   if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;
+  if (a.n_jframes && (a.kmask & 8)) {
+    auto* jframes = (const JFrame*)(ws + W.jframes);
+    auto* jd = (const JBlkDesc*)(ws + W.jblkd);
+    auto* jb = (JBlk*)(ws + W.jblk);
+    auto* jfin = ws + W.jfin;
+    auto* jp0 = (uint32_t*)(ws + W.jptr0);
+    auto* jp1 = (uint32_t*)(ws + W.jptr1);
+    auto* pend = (uint32_t*)(ws + W.jpend);
+    hipLaunchKernelGGL(zd_k_jsum, dim3(a.n_jblk), dim3(64), 0, s, a.src, (const FrameState*)fstate, blocks, comp,
+                       (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jb);
+    hipLaunchKernelGGL(zd_k_jprefix, dim3(a.n_jframes), dim3(64), 0, s, frames, fstate, jframes, jd, jb);
+    hipLaunchKernelGGL(zd_k_jscatter, dim3(a.n_jblk), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
+                       (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
+                       (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, jfin, jp0);
+    const uint64_t gw = (a.j_pieces + 255) / 256;
+    const dim3 gr((uint32_t)(gw < 8192 ? (gw ? gw : 1) : 8192));
+    for (uint32_t r = 1; r <= a.j_rounds; r++)
+      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes, a.j_pieces,
+                         jfin, (const uint32_t*)(r & 1 ? jp0 : jp1), r & 1 ? jp1 : jp0, pend, r,
+                         (uint32_t)(r == a.j_rounds));
+  }
+  if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;
   return hipGetLastError();
 }
 

@@ -22,6 +22,9 @@ struct LaunchArgs {
   uint32_t k4_grid = 0;    // cap on K4 workgroups (persistent over frames); 0 = one per frame
   bool overlap = false;    // K4 of frames [0, n_frames_a) on aux beside K3 of the rest
   uint32_t n_frames_a = 0, n_seq_a = 0;   // list_seq[0, n_seq_a) = the blocks of those frames
+  uint32_t n_jframes = 0, n_jblk = 0;      // K4J frames / their blocks
+  uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
+  uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
@@ -35,7 +38,7 @@ hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* 
 hipError_t launch_xxh64(const uint8_t* base, const uint64_t* d_off, const uint64_t* d_len, uint32_t n,
                         uint64_t* d_hash, hipStream_t s);
 
-constexpr int N_KERNELS = 5;
+constexpr int N_KERNELS = 6;
 constexpr uint32_t K4F_CAP = 128u << 10;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];
 

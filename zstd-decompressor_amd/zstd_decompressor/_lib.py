@@ -46,6 +46,13 @@ class PlanInfo(C.Structure):
                 ("device_ns", C.c_uint64)]
 
 
+class GatherResult(C.Structure):
+    _fields_ = [("total_len", C.c_uint64), ("status", C.c_int32), ("failed_rank", C.c_int32),
+                ("first_error_frame", C.c_int64)]
+
+
+COMM_ID_BYTES = 128
+
 # every entry point declared in include/zd.h: name -> (restype, argtypes)
 _u8p, _sz, _szp, _vp = C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_size_t), C.c_void_p
 SIGNATURES = {
@@ -69,6 +76,15 @@ SIGNATURES = {
                                        _sz, _vp, _sz]),
     "zd_context_decoded": (C.c_int, [_vp, _vp, _sz, _szp]),
     "zd_context_offsets": (C.c_int, [_vp, C.POINTER(C.c_uint64)]),
+    "zd_shard_partition": (C.c_int, [C.POINTER(C.c_uint64), _sz, C.c_int, _szp]),
+    "zd_shard_range": (C.c_int, [_vp, _sz, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "zd_comm_unique_id": (C.c_int, [_vp]),
+    "zd_comm_create": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "zd_comm_destroy": (None, [_vp]),
+    "zd_comm_gather": (C.c_int, [_vp, _vp, C.c_uint64, C.c_int32, C.c_int64, _vp, C.c_uint64,
+                                 C.POINTER(GatherResult), _vp]),
+    "zd_decode_sharded": (C.c_int, [_vp, _vp, _sz, C.c_uint32, _vp, C.c_uint64, C.POINTER(GatherResult), _vp]),
 }
 
 _lib = None
@@ -80,6 +96,16 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C zstd-decompressor_amd` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
+        # One HIP runtime per process: PyTorch-ROCm ships its own
+        # libamdhip64 (soname libamdhip64.so.7, loaded as "libamdhip64.so"),
+        # and libzd's dependency on libamdhip64.so.7 binds to whichever copy
+        # is already loaded.  Loading PyTorch's first keeps device pointers,
+        # streams and graphs from torch valid in libzd; loading libzd first
+        # would leave torch a second runtime that finds no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
@@ -124,3 +150,5 @@ RESERVED_BLOCK_TYPE = -50
 UNRECOGNIZED_MAGIC, FRAME_RESERVED_SET, MISSING_CHECKSUM, WINDOW_SIZE_TOO_BIG = -60, -61, -64, -66
 REF_PANIC, OUT_OF_DOMAIN, DST_TOO_SMALL, INVALID_ARG, HIP, NO_MEMORY, NOT_DECODED = -90, -91, -92, -93, -94, -95, -96
 F_SKIPPABLE = 1
+F_BLOCK_PARALLEL = 2   # every frame with a compressed block -> K4J (block-parallel execute)
+F_FRAME_SERIAL = 4     # no frame -> K4J

@@ -41,16 +41,17 @@ def decompress(data: bytes, print_skippable: bool = False) -> bytes:
     return bytes(out[: ol.value])
 
 
-def decompress_status(data: bytes, print_skippable: bool = False):
-    """(status, output of the frames before the first failure)."""
+def decompress_status(data: bytes, print_skippable: bool = False, flags: int = 0):
+    """(status, output of the frames before the first failure).  flags: extra
+    zd_plan flags (_lib.F_BLOCK_PARALLEL / F_FRAME_SERIAL pick the executor)."""
     L = _lib.lib()
     p, n, keep = _lib.buf(data)
-    plan = Plan(data, print_skippable)
+    plan = Plan(data, print_skippable, flags)
     cap = max(plan.info.out_bytes, 1)
     plan.close()
     out = (C.c_uint8 * cap)()
     ol = C.c_size_t()
-    st = L.zd_decompress(p, n, out, cap, C.byref(ol), _lib.F_SKIPPABLE if print_skippable else 0)
+    st = L.zd_decompress(p, n, out, cap, C.byref(ol), (_lib.F_SKIPPABLE if print_skippable else 0) | flags)
     if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
         _lib.check(st, "zd_decompress")
     return st, bytes(out[: min(ol.value, cap)])
@@ -59,12 +60,13 @@ def decompress_status(data: bytes, print_skippable: bool = False):
 class Plan:
     """zd_plan: host index + device workspace for one byte range of frames."""
 
-    def __init__(self, data: bytes, print_skippable: bool = False):
+    def __init__(self, data: bytes, print_skippable: bool = False, flags: int = 0):
         L = _lib.lib()
         self._data = data
         p, n, self._keep = _lib.buf(data)
         h = C.c_void_p()
-        _lib.check(L.zd_plan_create(p, n, _lib.F_SKIPPABLE if print_skippable else 0, C.byref(h)), "zd_plan_create")
+        _lib.check(L.zd_plan_create(p, n, (_lib.F_SKIPPABLE if print_skippable else 0) | flags, C.byref(h)),
+                   "zd_plan_create")
         self._h = h
         self.info = PlanInfo()
         _lib.check(L.zd_plan_info_get(h, C.byref(self.info)), "zd_plan_info_get")

@@ -32,13 +32,60 @@ def partition(sizes: Sequence[int], world: int) -> List[Tuple[int, int]]:
     cuts = [0]
     for k in range(1, world):
         # first item boundary whose prefix reaches k/world of the bytes
-        c = bisect.bisect_left(prefix, total * k / world)
+        c = bisect.bisect_left(prefix, -(-total * k // world))
         if n >= world:                       # leave one item for each remaining rank
             c = max(c, cuts[-1] + 1)
             c = min(c, n - (world - k))
         cuts.append(min(max(c, cuts[-1]), n))
     cuts.append(n)
     return [(cuts[k], cuts[k + 1]) for k in range(world)]
+
+
+def partition_native(sizes: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """The same cut through the C ABI (zd_shard_partition), which a host
+    binding (e.g. the reference's Rust CLI) calls."""
+    import ctypes as C
+    from . import _lib
+    arr = (C.c_uint64 * max(len(sizes), 1))(*sizes)
+    cuts = (C.c_size_t * (world + 1))()
+    _lib.check(_lib.lib().zd_shard_partition(arr, len(sizes), world, cuts), "zd_shard_partition")
+    return [(cuts[k], cuts[k + 1]) for k in range(world)]
+
+
+class Comm:
+    """zd_comm: libzd's own RCCL communicator (one GPU per rank).  The id is
+    made on rank 0 and broadcast over an initialised torch.distributed group."""
+
+    def __init__(self, rank: int, world: int, device, group=None):
+        import ctypes as C
+        import torch.distributed as dist
+        from . import _lib
+        L = _lib.lib()
+        idb = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+        if rank == 0:
+            _lib.check(L.zd_comm_unique_id(idb), "zd_comm_unique_id")
+        t = torch.tensor(list(idb), dtype=torch.uint8, device=device)
+        dist.broadcast(t, 0, group=group)
+        idb = (C.c_uint8 * _lib.COMM_ID_BYTES)(*t.cpu().tolist())
+        h = C.c_void_p()
+        _lib.check(L.zd_comm_create(idb, world, rank, C.byref(h)), "zd_comm_create")
+        self._h, self.rank, self.world = h, rank, world
+
+    def gather(self, d_local: int, length: int, status: int, first_error_frame: int, d_root: int,
+               root_cap: int, stream: int = 0):
+        """zd_comm_gather -> (call status, GatherResult)."""
+        import ctypes as C
+        from . import _lib
+        res = _lib.GatherResult()
+        st = _lib.lib().zd_comm_gather(self._h, C.c_void_p(d_local), length, status, first_error_frame,
+                                       C.c_void_p(d_root), root_cap, C.byref(res), C.c_void_p(stream))
+        return st, res
+
+    def close(self):
+        if getattr(self, "_h", None):
+            from . import _lib
+            _lib.lib().zd_comm_destroy(self._h)
+            self._h = None
 
 
 def shard_of(frames: Sequence[dict], rank: int, world: int) -> Tuple[int, int, int, int]:
@@ -83,21 +130,44 @@ def gather_to_root(local: torch.Tensor, length: int, rank: int, world: int, grou
     return None
 
 
+def global_status(status: int, first_frame: int, rank: int, world: int, device, group=None):
+    """The whole input's outcome from every rank's own one, on every rank.
+
+    The reference's CLI stops at the first frame that fails and keeps the
+    frames before it (src/main.rs:43-53, FrameIterator frame.rs:94-99); ranks
+    hold contiguous frame ranges in order, so that frame is the first failing
+    one of the lowest failing rank.  Returns (status, first_error_frame or -1,
+    failing rank or world): ranks after the failing one contribute nothing."""
+    if world == 1:
+        return status, first_frame if status else -1, 0 if status else world
+    import torch.distributed as dist
+    mine = torch.tensor([status, first_frame], dtype=torch.int64, device=device)
+    alls = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(alls, mine, group=group)
+    for r, t in enumerate(alls):
+        st, ff = (int(x) for x in t.tolist())
+        if st != 0:
+            return st, ff, r
+    return 0, -1, world
+
+
 def decode_sharded(data: bytes, rank: int, world: int, device: torch.device, group=None,
                    gather: bool = True):
     """Decode this rank's share of the frames of `data` on `device` (one GPU
     per rank) and optionally gather the whole output on rank 0.
 
     Returns (status, local_output_tensor, local_length, gathered_or_None).
-    The status is this rank's zd_plan_results status (0 = OK)."""
+    status is the whole input's (global_status): a failure on any rank fails
+    every rank, and the gathered output stops at the first failing frame,
+    keeping the frames before it, like the reference CLI."""
     from .batch import Plan, frames_index
     frames, _, st, _ = frames_index(data)
     if st != 0:
         raise ValueError(f"frame index failed with status {st}")
-    sb, se, _, _ = shard_of(frames, rank, world)
+    sb, se, fb, _ = shard_of(frames, rank, world)
     part = data[sb:se]
     length = 0
-    status = 0
+    status, first = 0, -1
     local = torch.empty(1, dtype=torch.uint8, device=device)
     if part:
         plan = Plan(part)
@@ -108,7 +178,21 @@ def decode_sharded(data: bytes, rank: int, world: int, device: torch.device, gro
         s = torch.cuda.current_stream(device).cuda_stream
         plan.decode_async(d_src.data_ptr(), local.data_ptr(), cap, s)
         torch.cuda.synchronize(device)
-        status, length, _, _, _ = plan.results(local.data_ptr(), s)
+        status, length, _, _, first = plan.results(local.data_ptr(), s)
         plan.close()
+    gst, _, length, gathered = collect(local, length, status, fb + first if status else -1, rank, world,
+                                       group, gather)
+    return gst, local, length, gathered
+
+
+def collect(local: torch.Tensor, length: int, status: int, first_frame: int, rank: int, world: int,
+            group=None, gather: bool = True):
+    """Every rank's decode outcome -> (global status, first error frame,
+    this rank's output length after the cut, gathered output on rank 0 or
+    None).  A rank after the first failing one outputs nothing; the failing
+    rank keeps the frames before its failure (its zd_plan_results length)."""
+    gst, gfirst, frank = global_status(status, first_frame, rank, world, local.device, group)
+    if rank > frank:
+        length = 0
     gathered = gather_to_root(local, length, rank, world, group) if gather else None
-    return status, local, length, gathered
+    return gst, gfirst, length, gathered
