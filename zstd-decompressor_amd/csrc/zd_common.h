@@ -109,10 +109,11 @@ ZD_HD inline uint32_t k3f_entry(uint32_t e, int k, int al) {
 // ---------------------------------------------------------------------------
 constexpr uint32_t DIRECT_GIANT = (1u << 29) - 1;
 // Output bounds per executor: the streaming K4 keeps int32 frame positions,
-// K4J u32 ones; a frame with sequences above both is outside the GPU path's
-// domain (ZD_E_OUT_OF_DOMAIN; the reference's own limit is the 8 MiB window).
+// K4J 31-bit ones in its state words; a frame with sequences above both is
+// outside the GPU path's domain (ZD_E_OUT_OF_DOMAIN; the reference's own
+// limit is the 8 MiB window).
 constexpr uint64_t K4_MAX_FRAME_OUT = 0x7FFF0000ull;
-constexpr uint64_t K4J_MAX_FRAME_OUT = 0xFFFF0000ull;
+constexpr uint64_t K4J_MAX_FRAME_OUT = 0x7FFF0000ull;   // positions below J_FINAL (zd_kernels.hip K4J)
 constexpr uint64_t OFF_HUGE = ~0ull >> 1;        // a giant offset (never <= a decoded length)
 
 ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t ofv) {
@@ -361,17 +362,18 @@ struct FrameState {
 
 // ---------------------------------------------------------------------------
 // K4J: frames of many blocks executed block-parallel (zd_kernels.hip K4J).
-// A frame is laid out as per-byte state in three arrays of its own region
-// [base, base + cap): fin (u8: 0 = final from the scatter, r = made final in
-// pointer-jumping round r, J_PENDING = a match byte still to resolve) and two
-// u32 pointer arrays (the frame position each pending byte copies from), used
-// alternately by the rounds.
+// A frame's bytes are laid out as one u32 state word each in its region
+// [base, base + cap) of the state array: J_FINAL | byte for a byte whose
+// value is known, else the frame position the byte copies (a pointer the
+// pointer-jumping rounds follow, in place; every version of a word is true
+// of the byte, so the rounds need no ordering between lanes).
 // ---------------------------------------------------------------------------
-constexpr uint8_t J_PENDING = 255;
+constexpr uint32_t J_FINAL = 1u << 31;
 constexpr int J_MAX_ROUNDS = 40;
+constexpr uint32_t J_SEG = 1024;           // sequences per K4J scatter segment (one wave each)
 struct JFrame {
-  uint64_t base;           // byte index of the frame's region in fin / the pointer arrays
-  uint64_t cap;            // bytes of the region (>= the frame's capacity)
+  uint64_t base;           // word index of the frame's region in the state array
+  uint64_t cap;            // words of the region (>= the frame's capacity)
   uint64_t piece0;         // first 16-byte piece of the frame in the rounds' piece numbering
   uint32_t frame;          // plan frame index
   uint32_t jb0, njb;       // its blocks: JBlkDesc / JBlk [jb0, jb0 + njb)
@@ -381,15 +383,25 @@ struct JBlkDesc {          // static, from the host
   uint32_t block;          // BlockRec index
   uint32_t jframe;         // JFrame index
   uint32_t j;              // block index inside the frame
-  uint32_t pad;
+  uint32_t seg0;           // its scatter segments: JSeg [seg0, seg0 + max(1, ceil(nseq / J_SEG)))
 };
 struct JBlk {              // device: K4J pass results per block
   uint64_t out_start;      // frame position of the block's first output byte
   uint64_t size;           // output bytes (literals + match lengths)
   uint64_t rep_in[3];      // repeat offsets before the block (concrete)
-  uint64_t map[3];         // the block's repeat-offset map (zd_kernels.hip j_rep codes)
+  uint64_t map[3];         // the block's repeat-offset map (jr codes)
   uint32_t dead;           // 1: not executed (a failure before it, or past the capacity)
   uint32_t pad;
+};
+struct JSeg {              // device: where segment k of a block starts (KJ1 -> KJ3)
+  uint64_t out_rel;        // output bytes of the block's sequences before the segment
+  uint64_t map[3];         // repeat offsets there, as jr codes of the block's incoming ones
+  uint32_t lit_rel;        // literals consumed before it
+  uint32_t pad;
+};
+struct JSegDesc {          // static: the scatter's work list
+  uint32_t jblk;           // JBlk index
+  uint32_t k;              // segment of the block
 };
 
 // Workspace carve-up, all offsets in bytes from the workspace base.
@@ -398,8 +410,8 @@ struct Workspace {
   uint64_t list_tables, list_huf, list_seq, list_k4f;   // u32 work lists
   uint64_t copies;                                      // CopyDesc[] for K0
   uint64_t lits, seqs, luts, fses;
-  uint64_t jframes, jblkd, jblk, jpend;                 // K4J descriptors / state / round counters
-  uint64_t jfin, jptr0, jptr1;                          // K4J per-byte arrays
+  uint64_t jframes, jblkd, jblk, jseg, jsegd, jpend;    // K4J descriptors / state / round counters
+  uint64_t jst;                                         // K4J per-byte state words
   uint64_t total;
 };
 

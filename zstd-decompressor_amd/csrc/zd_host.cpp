@@ -317,8 +317,9 @@ struct zd_plan {
   std::vector<FrameState> fstate0;
   std::vector<uint32_t> list_tables, list_huf, list_seq, list_k4f;
   std::vector<CopyDesc> copies;         // K0 pieces
-  std::vector<JFrame> jframes;          // K4J frames and their blocks
+  std::vector<JFrame> jframes;          // K4J frames, their blocks and the scatter's segments
   std::vector<JBlkDesc> jblkd;
+  std::vector<JSegDesc> jsegd;
   uint64_t j_bytes = 0, j_pieces = 0;
   uint32_t j_rounds = 0;
   std::vector<uint64_t> frame_cap_off;   // output offset per frame (capacity layout)
@@ -369,7 +370,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   uint32_t lut_slots = 0, fse_slots = 0;
   bool exact = true;
   P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
-  P->frame_cap_off.clear(); P->jframes.clear(); P->jblkd.clear();
+  P->frame_cap_off.clear(); P->jframes.clear(); P->jblkd.clear(); P->jsegd.clear();
   static const char* k4f_env = getenv("ZD_K4F");
   const bool k4f_on = k4f_env ? atoi(k4f_env) == 1
                               : P->frames.size() >= K4F_AUTO_MIN_FRAMES && P->frames.size() <= K4F_AUTO_MAX_FRAMES;
@@ -496,9 +497,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     if (to_j) {
       fd.lds = 2;
       JFrame jf{};
-      // the region's byte index has the output offset's alignment mod 16, so
-      // 16-byte pieces of the output, fin and the pointer arrays line up
-      jf.base = align_up(j_base, 16) + (out_off & 15);
+      jf.base = align_up(j_base, 16);          // word index: frame pieces of 16 words are 64-byte lines
       jf.cap = cap;
       jf.piece0 = j_pieces;
       jf.frame = (uint32_t)fi;
@@ -510,9 +509,12 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
         d.block = fd.first_block + k;
         d.jframe = (uint32_t)P->jframes.size();
         d.j = k;
-        P->jblkd.push_back(d);
+        d.seg0 = (uint32_t)P->jsegd.size();
         const BlockRec& br = P->blocks[fd.first_block + k];
-        if (br.comp >= 0) nseq += P->comps[(size_t)br.comp].nseq;
+        const uint32_t bn = br.comp >= 0 ? P->comps[(size_t)br.comp].nseq : 0;
+        nseq += bn;
+        for (uint32_t g = 0; g == 0 || g * J_SEG < bn; g++) P->jsegd.push_back(JSegDesc{(uint32_t)P->jblkd.size(), g});
+        P->jblkd.push_back(d);
       }
       j_maxseq = std::max(j_maxseq, nseq);
       j_base = jf.base + cap + 16;
@@ -586,10 +588,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.jframes = carve(sizeof(JFrame) * std::max<size_t>(P->jframes.size(), 1));
   W.jblkd = carve(sizeof(JBlkDesc) * std::max<size_t>(P->jblkd.size(), 1));
   W.jblk = carve(sizeof(JBlk) * std::max<size_t>(P->jblkd.size(), 1));
+  W.jseg = carve(sizeof(JSeg) * std::max<size_t>(P->jsegd.size(), 1));
+  W.jsegd = carve(sizeof(JSegDesc) * std::max<size_t>(P->jsegd.size(), 1));
   W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
-  W.jfin = carve(P->j_bytes + 64);
-  W.jptr0 = carve(4 * P->j_bytes + 64);
-  W.jptr1 = carve(4 * P->j_bytes + 64);
+  W.jst = carve(4 * P->j_bytes + 64);
   W.total = o;
 
   zd_plan_info& I = P->info;
@@ -628,6 +630,7 @@ int upload_plan(zd_plan* P) {
   if (int r = up(P->W.frame_state0, P->fstate0.data(), P->fstate0.size() * sizeof(FrameState))) return r;
   if (int r = up(P->W.jframes, P->jframes.data(), P->jframes.size() * sizeof(JFrame))) return r;
   if (int r = up(P->W.jblkd, P->jblkd.data(), P->jblkd.size() * sizeof(JBlkDesc))) return r;
+  if (int r = up(P->W.jsegd, P->jsegd.data(), P->jsegd.size() * sizeof(JSegDesc))) return r;
   if (!P->info.out_exact) {
     P->staging_bytes = P->info.out_bytes;
     HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
@@ -915,6 +918,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_copies = (uint32_t)P->copies.size();
   a.n_jframes = (uint32_t)P->jframes.size();
   a.n_jblk = (uint32_t)P->jblkd.size();
+  a.n_jseg = (uint32_t)P->jsegd.size();
   a.j_rounds = P->j_rounds;
   a.j_pieces = P->j_pieces;
   a.stream = s;

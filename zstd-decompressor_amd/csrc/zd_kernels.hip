@@ -2270,24 +2270,26 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 // dependencies apart:
 //   KJ1 zd_k_jsum     one wave per block: the block's output size (literals +
 //                     match lengths) and its repeat-offset map (decode_offset
-//                     as a function of the three offsets coming in, jr codes)
+//                     as a function of the three offsets coming in, jr codes),
+//                     with a checkpoint every J_SEG sequences (JSeg)
 //   KJ2 zd_k_jprefix  one wave per frame: scans over the blocks give each
 //                     block's output position and the concrete repeat offsets
 //                     entering it; the capacity check
-//   KJ3 zd_k_jscatter one wave per block: the sequences with concrete offsets
-//                     and the reference's checks; literal bytes are written
-//                     final, every match byte as a pointer to the frame
-//                     position it copies (q - off + j mod off: the period of an
-//                     overlapping match, as the reference's byte-by-byte push)
-//   KJ4 zd_k_jround   pointer jumping over the match bytes: a byte whose
-//                     source is final copies it, else takes over its source's
-//                     pointer, so round r resolves chains of up to 2^r - 1
-//                     hops.  A chain ends at a literal after at most one hop
-//                     per earlier match: ceil(log2(matches + 1)) rounds
-//                     finish (launched with an early exit once nothing is
-//                     pending).
-// Per byte of these frames: fin (u8) and two u32 pointer arrays, used
-// alternately by the rounds (zd_common.h JFrame).
+//   KJ3 zd_k_jscatter one wave per J_SEG sequences: concrete offsets from the
+//                     checkpoint, the reference's checks; every literal byte's
+//                     state word is J_FINAL | byte, every match byte's the
+//                     frame position it copies (q - off + j mod off: within
+//                     the period of an overlapping match, as the reference's
+//                     byte-by-byte push)
+//   KJ4 zd_k_jround   pointer jumping, in place: S[p] = S[S[p]] for every
+//                     pending word (a final source hands over its byte, a
+//                     pending one its pointer), so round r resolves chains of
+//                     up to 2^r - 1 hops.  A chain ends at a literal after at
+//                     most one hop per earlier match: ceil(log2(matches + 1))
+//                     rounds finish (launched with an early exit once nothing
+//                     is pending).  Any version of a word is true of its byte,
+//                     so lanes need no ordering within a round.
+//   KJ5 zd_k_jemit    the bytes of the state words -> the output
 // ---------------------------------------------------------------------------
 __device__ inline bool j_live(uint64_t key, uint32_t j) {
   // a parse error ends the frame before any block decodes (frame.rs:198-230);
@@ -2439,7 +2441,8 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
                                                 const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp,
                                                 const CompState* __restrict__ cstate, const uint64_t* __restrict__ seqs,
                                                 const uint16_t* __restrict__ fses, const JFrame* __restrict__ jframes,
-                                                const JBlkDesc* __restrict__ jd, JBlk* __restrict__ jb) {
+                                                const JBlkDesc* __restrict__ jd, JBlk* __restrict__ jb,
+                                                JSeg* __restrict__ jseg) {
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
   const int lane = threadIdx.x;
   const uint32_t e = blockIdx.x;
@@ -2449,6 +2452,11 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
   uint64_t rep[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
   uint64_t size = 0;
   uint32_t dead = j_live(key0, D.j) ? 0u : 1u;
+  if (lane == 0) {                                  // segment 0 starts the block
+    JSeg g{};
+    g.map[0] = rep[0]; g.map[1] = rep[1]; g.map[2] = rep[2];
+    jseg[D.seg0] = g;
+  }
   if (!dead && B.type != 2) {
     size = B.size;                                  // raw / RLE (block.rs:76-79)
   } else if (!dead) {
@@ -2458,23 +2466,33 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
       dead = 1;
     } else {
       const uint32_t nl = (C.lit_type == LIT_RAW || C.lit_type == LIT_RLE) ? C.lit_regen : CS.lit_count;
-      uint64_t summ = 0;
+      uint64_t out_rel = 0;                         // uniform
+      uint32_t lit_rel = 0;
       const uint32_t n = C.nseq;
       if (n) {
         j_stab(stab, C, comp, cstate, fses, lane);
         JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n};
         R.start(0, lane);
         for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+          if (s0 && s0 % J_SEG == 0 && lane == 0) {  // a checkpoint for KJ3's segment
+            JSeg g{};
+            g.out_rel = out_rel;
+            g.map[0] = rep[0]; g.map[1] = rep[1]; g.map[2] = rep[2];
+            g.lit_rel = lit_rel;
+            jseg[D.seg0 + s0 / J_SEG] = g;
+          }
           const int k = (int)min(64u, n - s0);
           uint32_t ll = 0, ml = 0, ofv = 4;
           if (lane < k) j_values(R.recA, R.winA, stab, ll, ml, ofv);
           R.next(s0, lane);
-          summ += ml;
           int bl, bc;
           (void)j_offsets<true>(ofv, ll, k, rep, &bl, &bc);
+          const uint32_t it = wave_scan_incl(ll + ml), il = wave_scan_incl(ll);
+          out_rel += (uint32_t)__builtin_amdgcn_readlane((int)it, 63);
+          lit_rel += (uint32_t)__builtin_amdgcn_readlane((int)il, 63);
         }
       }
-      size = nl + wave_sum_u64(summ);
+      size = (uint64_t)nl + out_rel - lit_rel;      // literals + match lengths
     }
   }
   if (lane == 0) {
@@ -2547,46 +2565,58 @@ __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__
 }
 
 typedef __attribute__((address_space(1))) u32x4a1 g_u32x4a1;
-// Bytes [x0, x1) of a 16-byte piece (x1 - x0 <= 16, b = byte index in the
-// piece) go to p + x0: one 16-byte store for a whole piece, else byte by byte
-// (a partial piece shares its aligned 16 bytes with another lane's).
+// Bytes [0, n) of a 16-byte piece (n <= 16) to p: one 16-byte store for a
+// whole piece, else byte by byte (a partial piece shares its aligned 16
+// bytes with another lane's).
 __device__ inline void j_store16(uint8_t* p, const u32x4& v, uint32_t n) {
   if (n == 16) { *(g_u32x4a1*)p = v; return; }
 #pragma unroll
   for (uint32_t b = 0; b < 16; b++)
     if (b < n) p[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
 }
+// Words [0, n) of 16 state words to p (n <= 16): four 16-byte stores, or one by one.
+__device__ inline void j_store_words(uint32_t* p, const uint32_t w[16], uint32_t n) {
+  if (n == 16) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) *(g_u32x4a1*)(p + 4 * q) = (u32x4){w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+    return;
+  }
+#pragma unroll
+  for (uint32_t b = 0; b < 16; b++)
+    if (b < n) p[b] = w[b];
+}
+__device__ inline void j_load_words(const uint32_t* p, uint32_t w[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const u32x4 t = *(const g_u32x4a1*)(p + 4 * q);
+    w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+  }
+}
 
 // n literal bytes from s (HBM) or the fill byte at frame position P0: final.
-__device__ void j_fill_lits(uint8_t* out, uint8_t* fin, uint32_t P0, uint32_t n, const uint8_t* s, uint32_t fill,
-                            int lane) {
+// 16-byte pieces aligned in the state array's 64-byte lines.
+__device__ void j_fill_lits(uint32_t* st, uint32_t P0, uint32_t n, const uint8_t* s, uint32_t fill, int lane) {
   if (!n) return;
-  const uint32_t g = (uint32_t)((16 - ((uintptr_t)(out + P0) & 15)) & 15);
+  const uint32_t g = (16 - (P0 & 15)) & 15;
   const uint32_t np = n > g ? 1 + (n - g + 15) / 16 : 1;
-  const u32x4 f4 = (u32x4){fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u, fill * 0x01010101u};
-  const u32x4 z4 = (u32x4){0u, 0u, 0u, 0u};
   for (uint32_t pi = lane; pi < np; pi += 64) {
     const uint32_t x0 = pi == 0 ? 0 : g + 16 * (pi - 1);
     const uint32_t x1 = pi == 0 ? min(g, n) : min(n, g + 16 * pi);
     if (x0 >= x1) continue;
-    u32x4 v = f4;
-    if (s) {
-      if (x1 - x0 == 16) {
-        v = ldg16(s + x0);
-      } else {
-        v = z4;
+    uint32_t w[16];
+    if (s && x1 - x0 == 16) {
+      const u32x4 v = ldg16(s + x0);
 #pragma unroll
-        for (uint32_t b = 0; b < 16; b++)
-          if (x0 + b < x1) v[b >> 2] |= (uint32_t)s[x0 + b] << (8 * (b & 3));
-      }
+      for (uint32_t b = 0; b < 16; b++) w[b] = J_FINAL | ((v[b >> 2] >> (8 * (b & 3))) & 255);
+    } else {
+#pragma unroll
+      for (uint32_t b = 0; b < 16; b++) w[b] = J_FINAL | (s ? (x0 + b < x1 ? s[x0 + b] : 0u) : fill);
     }
-    j_store16(out + P0 + x0, v, x1 - x0);
-    j_store16(fin + P0 + x0, z4, x1 - x0);
+    j_store_words(st + P0 + x0, w, x1 - x0);
   }
 }
 
-__global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ src, uint8_t* outbase,
-                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
+__global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ src, FrameState* fstate,
                                                     const BlockRec* __restrict__ blocks,
                                                     const CompBlock* __restrict__ comp,
                                                     const CompState* __restrict__ cstate,
@@ -2594,22 +2624,21 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
                                                     const uint16_t* __restrict__ fses,
                                                     const JFrame* __restrict__ jframes,
                                                     const JBlkDesc* __restrict__ jd, const JBlk* __restrict__ jb,
-                                                    uint8_t* jfin, uint32_t* jptr) {
+                                                    const JSeg* __restrict__ jseg, const JSegDesc* __restrict__ jsd,
+                                                    uint32_t* jst) {
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
   __shared__ uint32_t sa[65], sll[64], soff[64], slp[64];
   const int lane = threadIdx.x;
-  const uint32_t e = blockIdx.x;
+  const JSegDesc SD = jsd[blockIdx.x];
+  const uint32_t e = SD.jblk;
   if (jb[e].dead) return;
   const JBlkDesc D = jd[e];
   const JFrame JF = jframes[D.jframe];
-  const FrameDesc F = frames[JF.frame];
-  uint8_t* out = outbase + F.out;
-  uint8_t* fin = jfin + JF.base;
-  uint32_t* ptr = jptr + JF.base;
+  uint32_t* st = jst + JF.base;
   const BlockRec B = blocks[D.block];
   uint32_t pos = (uint32_t)jb[e].out_start;
   if (B.type != 2) {
-    j_fill_lits(out, fin, pos, B.size, B.type == 1 ? nullptr : src + B.src, B.rle, lane);
+    j_fill_lits(st, pos, B.size, B.type == 1 ? nullptr : src + B.src, B.rle, lane);
     return;
   }
   const CompBlock C = comp[B.comp];
@@ -2619,15 +2648,19 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
   if (C.lit_type == LIT_RAW) { lsrc = src + C.src + C.lit_data; nl = C.lit_regen; }
   else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle; nl = C.lit_regen; }
   else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
-  uint32_t lit_cursor = 0;
+  const JSeg G = jseg[D.seg0 + SD.k];
+  const uint64_t rin[3] = {jb[e].rep_in[0], jb[e].rep_in[1], jb[e].rep_in[2]};
+  uint64_t rep[3] = {jr_apply(G.map[0], rin), jr_apply(G.map[1], rin), jr_apply(G.map[2], rin)};
+  pos += (uint32_t)G.out_rel;
+  uint32_t lit_cursor = G.lit_rel;
   const uint32_t n = C.nseq;
-  if (n) {
-    uint64_t rep[3] = {jb[e].rep_in[0], jb[e].rep_in[1], jb[e].rep_in[2]};
+  const uint32_t sb = SD.k * J_SEG, se = min(n, sb + J_SEG);
+  if (se > sb) {
     j_stab(stab, C, comp, cstate, fses, lane);
-    JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n};
-    R.start(0, lane);
-    for (uint32_t s0 = 0; s0 < n; s0 += 64) {
-      const int k = (int)min(64u, n - s0);
+    JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, se};
+    R.start(sb, lane);
+    for (uint32_t s0 = sb; s0 < se; s0 += 64) {
+      const int k = (int)min(64u, se - s0);
       const bool valid = lane < k;
       uint32_t ll = 0, ml = 0, ofv = 4;
       if (valid) j_values(R.recA, R.winA, stab, ll, ml, ofv);
@@ -2660,8 +2693,8 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
       if (lane == 0) sa[k] = T;
       k4_sync();
       // the batch's bytes [pos, pos + T) in 16-byte pieces (aligned in the
-      // output): the sequence of each byte by a search of the batch's starts
-      const uint32_t g = (uint32_t)((16 - ((uintptr_t)(out + pos) & 15)) & 15);
+      // state array): the sequence of each byte by a search of the starts
+      const uint32_t g = (16 - (pos & 15)) & 15;
       const uint32_t np = T > g ? 1 + (T - g + 15) / 16 : 1;
       for (uint32_t pi = lane; pi < np; pi += 64) {
         const uint32_t x0 = pi == 0 ? 0 : g + 16 * (pi - 1);
@@ -2669,134 +2702,118 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
         if (x0 >= x1) continue;
         int i = 0;
 #pragma unroll
-        for (int st = 32; st; st >>= 1)
-          if (i + st < k && sa[i + st] <= x0) i += st;
+        for (int stp = 32; stp; stp >>= 1)
+          if (i + stp < k && sa[i + stp] <= x0) i += stp;
         uint32_t a = sa[i], nx = sa[i + 1], l = sll[i], o = soff[i], lp = slp[i];
-        u32x4 vo = (u32x4){0u, 0u, 0u, 0u}, vf = vo;
-        uint32_t pw[16];
+        uint32_t w[16];
 #pragma unroll
         for (uint32_t b = 0; b < 16; b++) {
           const uint32_t x = x0 + b;
-          pw[b] = 0;
+          w[b] = 0;
           if (x < x1) {
             while (x >= nx) { i++; a = nx; nx = sa[i + 1]; l = sll[i]; o = soff[i]; lp = slp[i]; }
             const uint32_t rel = x - a;
             if (rel < l) {
-              const uint32_t byte = lsrc ? lsrc[lp + rel] : lfill;
-              vo[b >> 2] |= byte << (8 * (b & 3));
+              w[b] = J_FINAL | (lsrc ? (uint32_t)lsrc[lp + rel] : lfill);
             } else {
               const uint32_t jj = rel - l;
-              pw[b] = pos + a + l - o + (jj < o ? jj : jj % o);
-              vf[b >> 2] |= (uint32_t)J_PENDING << (8 * (b & 3));
+              w[b] = pos + a + l - o + (jj < o ? jj : jj % o);
             }
           }
         }
-        const uint32_t nb = x1 - x0;
-        j_store16(out + pos + x0, vo, nb);
-        j_store16(fin + pos + x0, vf, nb);
-        uint32_t* pp = ptr + pos + x0;
-        if (nb == 16) {
-#pragma unroll
-          for (int w = 0; w < 4; w++) *(g_u32x4a1*)(pp + 4 * w) = (u32x4){pw[4 * w], pw[4 * w + 1], pw[4 * w + 2], pw[4 * w + 3]};
-        } else {
-#pragma unroll
-          for (uint32_t b = 0; b < 16; b++)
-            if (b < nb) pp[b] = pw[b];
-        }
+        j_store_words(st + pos + x0, w, x1 - x0);
       }
       k4_sync();
       lit_cursor += Lsum;
       pos += T;
     }
   }
-  // leftover literals (decoding_context.rs:101-103)
-  if (lit_cursor < nl) j_fill_lits(out, fin, pos, nl - lit_cursor, lsrc ? lsrc + lit_cursor : nullptr, lfill, lane);
+  // leftover literals (decoding_context.rs:101-103), by the block's last segment
+  if (se == n && lit_cursor < nl)
+    j_fill_lits(st, pos, nl - lit_cursor, lsrc ? lsrc + lit_cursor : nullptr, lfill, lane);
 }
 
-// One pointer-jumping round over the K4J frames' bytes, 16 per thread.
-// Round r trusts fin values below r (bytes made final by an earlier launch,
-// whose output bytes are visible); a byte made final in this round reads as
-// pending, and its pointer (written by round r - 1) still holds.
-__global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const FrameDesc* __restrict__ frames,
-                                                   FrameState* fstate, const JFrame* __restrict__ jframes,
-                                                   uint32_t n_jframes, uint64_t n_pieces, uint8_t* jfin,
-                                                   const uint32_t* __restrict__ pa, uint32_t* __restrict__ pb,
+// The frame and 16-word piece of piece number pc (K4J rounds and emit).
+__device__ inline uint32_t j_frame_of(const JFrame* __restrict__ jframes, uint32_t n_jframes, uint64_t pc) {
+  uint32_t lo = 0, hi = n_jframes;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (jframes[mid].piece0 <= pc) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One pointer-jumping round over the K4J frames' state words, 16 per thread:
+// S[p] = S[S[p]] for each pending word.  A piece inside one match whose
+// source run is contiguous reads it with four 16-byte loads; otherwise one
+// gather per pending word.
+__global__ __launch_bounds__(256) void zd_k_jround(FrameState* fstate, const JFrame* __restrict__ jframes,
+                                                   uint32_t n_jframes, uint64_t n_pieces, uint32_t* jst,
                                                    uint32_t* pend, uint32_t r, uint32_t last) {
   if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
   uint32_t mine = 0;
   for (uint64_t pc = (uint64_t)blockIdx.x * 256 + threadIdx.x; pc < n_pieces; pc += (uint64_t)gridDim.x * 256) {
-    uint32_t lo = 0, hi = n_jframes;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (jframes[mid].piece0 <= pc) lo = mid;
-      else hi = mid;
-    }
-    const JFrame JF = jframes[lo];
+    const JFrame JF = jframes[j_frame_of(jframes, n_jframes, pc)];
     const FrameState* S = &fstate[JF.frame];
     if (S->key != KEY_NONE) continue;
     const uint64_t total = S->out_len;
     const uint64_t p0 = 16 * (pc - JF.piece0);
     if (p0 >= total) continue;
     const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
-    uint8_t* fin = jfin + JF.base;
-    u32x4 vf = *(g_u32x4a1*)(fin + p0);
-    uint32_t pm = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 16; b++)
-      pm |= (b < nb && ((vf[b >> 2] >> (8 * (b & 3))) & 255) == J_PENDING) ? (1u << b) : 0u;
-    if (!pm) continue;
-    uint8_t* out = outbase + frames[JF.frame].out;
-    const uint32_t* A = pa + JF.base;
-    uint32_t* Bp = pb + JF.base;
-    uint32_t q[16];
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const u32x4 t = *(const g_u32x4a1*)(A + p0 + 4 * w);
-      q[4 * w] = t.x; q[4 * w + 1] = t.y; q[4 * w + 2] = t.z; q[4 * w + 3] = t.w;
-    }
-    u32x4 vo = *(g_u32x4a1*)(out + p0);
-    uint32_t fs[16], os[16], ns[16];
+    uint32_t* st = jst + JF.base;
+    uint32_t w[16];
+    j_load_words(st + p0, w);
+    uint32_t pm = 0, contig = 1;
 #pragma unroll
     for (uint32_t b = 0; b < 16; b++) {
-      fs[b] = 0; os[b] = 0; ns[b] = 0;
-      if ((pm >> b) & 1) {
-        const uint32_t s = q[b] < total ? q[b] : 0;   // (always below p0 + b by construction)
-        fs[b] = fin[s];
-        os[b] = out[s];
-        ns[b] = A[s];
-      }
+      pm |= (b < nb && !(w[b] & J_FINAL)) ? (1u << b) : 0u;
+      contig &= (uint32_t)(w[b] == w[0] + b);
+    }
+    if (!pm) continue;
+    if (pm == 0xFFFFu && contig && w[0] + 16 <= total) {
+      j_load_words(st + w[0], w);                  // one contiguous source run
+    } else {
+      uint32_t v[16];
+#pragma unroll
+      for (uint32_t b = 0; b < 16; b++) v[b] = ((pm >> b) & 1) ? st[w[b] < total ? w[b] : 0] : w[b];
+#pragma unroll
+      for (uint32_t b = 0; b < 16; b++) w[b] = v[b];
     }
     uint32_t still = 0;
 #pragma unroll
-    for (uint32_t b = 0; b < 16; b++) {
-      if ((pm >> b) & 1) {
-        const uint32_t sh = 8 * (b & 3);
-        if (fs[b] < r) {
-          vo[b >> 2] = (vo[b >> 2] & ~(255u << sh)) | (os[b] << sh);
-          vf[b >> 2] = (vf[b >> 2] & ~(255u << sh)) | (r << sh);
-        } else {
-          q[b] = ns[b];
-          still |= 1u << b;
-        }
-      }
-    }
-    j_store16(out + p0, vo, nb);
-    j_store16(fin + p0, vf, nb);
+    for (uint32_t b = 0; b < 16; b++) still |= (b < nb && !(w[b] & J_FINAL)) ? 1u : 0u;
+    j_store_words(st + p0, w, nb);
     if (still) {
-      if (nb == 16) {
-#pragma unroll
-        for (int w = 0; w < 4; w++) *(g_u32x4a1*)(Bp + p0 + 4 * w) = (u32x4){q[4 * w], q[4 * w + 1], q[4 * w + 2], q[4 * w + 3]};
-      } else {
-#pragma unroll
-        for (uint32_t b = 0; b < 16; b++)
-          if ((still >> b) & 1) Bp[p0 + b] = q[b];
-      }
       mine++;
       if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
     }
   }
   const uint64_t bm = __ballot(mine != 0);
   if ((threadIdx.x & 63) == 0 && bm) atomicAdd(&pend[r], (uint32_t)__popcll(bm));
+}
+
+// The frames' bytes from their state words, 16 per thread (frames without a
+// failure only).
+__global__ __launch_bounds__(256) void zd_k_jemit(uint8_t* outbase, const FrameDesc* __restrict__ frames,
+                                                  const FrameState* __restrict__ fstate,
+                                                  const JFrame* __restrict__ jframes, uint32_t n_jframes,
+                                                  uint64_t n_pieces, const uint32_t* __restrict__ jst) {
+  for (uint64_t pc = (uint64_t)blockIdx.x * 256 + threadIdx.x; pc < n_pieces; pc += (uint64_t)gridDim.x * 256) {
+    const JFrame JF = jframes[j_frame_of(jframes, n_jframes, pc)];
+    const FrameState* S = &fstate[JF.frame];
+    if (S->key != KEY_NONE) continue;
+    const uint64_t total = S->out_len;
+    const uint64_t p0 = 16 * (pc - JF.piece0);
+    if (p0 >= total) continue;
+    const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
+    uint32_t w[16];
+    j_load_words(jst + JF.base + p0, w);
+    u32x4 v = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b++) v[b >> 2] |= (w[b] & 255) << (8 * (b & 3));
+    j_store16(outbase + frames[JF.frame].out + p0, v, nb);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2963,22 +2980,23 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     auto* jframes = (const JFrame*)(ws + W.jframes);
     auto* jd = (const JBlkDesc*)(ws + W.jblkd);
     auto* jb = (JBlk*)(ws + W.jblk);
-    auto* jfin = ws + W.jfin;
-    auto* jp0 = (uint32_t*)(ws + W.jptr0);
-    auto* jp1 = (uint32_t*)(ws + W.jptr1);
+    auto* jseg = (JSeg*)(ws + W.jseg);
+    auto* jsd = (const JSegDesc*)(ws + W.jsegd);
+    auto* jst = (uint32_t*)(ws + W.jst);
     auto* pend = (uint32_t*)(ws + W.jpend);
     hipLaunchKernelGGL(zd_k_jsum, dim3(a.n_jblk), dim3(64), 0, s, a.src, (const FrameState*)fstate, blocks, comp,
-                       (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jb);
+                       (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jb, jseg);
     hipLaunchKernelGGL(zd_k_jprefix, dim3(a.n_jframes), dim3(64), 0, s, frames, fstate, jframes, jd, jb);
-    hipLaunchKernelGGL(zd_k_jscatter, dim3(a.n_jblk), dim3(64), 0, s, a.src, a.out, frames, fstate, blocks, comp,
+    hipLaunchKernelGGL(zd_k_jscatter, dim3(a.n_jseg), dim3(64), 0, s, a.src, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
-                       (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, jfin, jp0);
+                       (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, (const JSeg*)jseg, jsd, jst);
     const uint64_t gw = (a.j_pieces + 255) / 256;
     const dim3 gr((uint32_t)(gw < 8192 ? (gw ? gw : 1) : 8192));
     for (uint32_t r = 1; r <= a.j_rounds; r++)
-      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes, a.j_pieces,
-                         jfin, (const uint32_t*)(r & 1 ? jp0 : jp1), r & 1 ? jp1 : jp0, pend, r,
+      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, fstate, jframes, a.n_jframes, a.j_pieces, jst, pend, r,
                          (uint32_t)(r == a.j_rounds));
+    hipLaunchKernelGGL(zd_k_jemit, gr, dim3(256), 0, s, a.out, frames, (const FrameState*)fstate, jframes,
+                       a.n_jframes, a.j_pieces, (const uint32_t*)jst);
   }
   if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;
   return hipGetLastError();

@@ -22,7 +22,7 @@ struct LaunchArgs {
   uint32_t k4_grid = 0;    // cap on K4 workgroups (persistent over frames); 0 = one per frame
   bool overlap = false;    // K4 of frames [0, n_frames_a) on aux beside K3 of the rest
   uint32_t n_frames_a = 0, n_seq_a = 0;   // list_seq[0, n_seq_a) = the blocks of those frames
-  uint32_t n_jframes = 0, n_jblk = 0;      // K4J frames / their blocks
+  uint32_t n_jframes = 0, n_jblk = 0, n_jseg = 0;   // K4J frames / their blocks / scatter segments
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
 };
