@@ -411,6 +411,7 @@ struct Workspace {
   uint64_t copies;                                      // CopyDesc[] for K0
   uint64_t lits, seqs, luts, fses;
   uint64_t jframes, jblkd, jblk, jseg, jsegd, jpend;    // K4J descriptors / state / round counters
+  uint64_t jdone;                                       // K4J: one byte per piece, 1 once emitted
   uint64_t jst;                                         // K4J per-byte state words
   uint64_t total;
 };

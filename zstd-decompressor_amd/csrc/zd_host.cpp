@@ -591,6 +591,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.jseg = carve(sizeof(JSeg) * std::max<size_t>(P->jsegd.size(), 1));
   W.jsegd = carve(sizeof(JSegDesc) * std::max<size_t>(P->jsegd.size(), 1));
   W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
+  W.jdone = carve(std::max<uint64_t>(j_pieces, 1));
   W.jst = carve(4 * P->j_bytes + 64);
   W.total = o;
 
@@ -903,7 +904,10 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->d_ws + P->W.frame_state0,
                         P->fstate0.size() * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
-  if (!P->jframes.empty()) HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
+  if (!P->jframes.empty()) {
+    HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
+    HIPCHK(hipMemsetAsync(P->d_ws + P->W.jdone, 0, std::max<uint64_t>(P->j_pieces, 1), s));
+  }
   LaunchArgs a{};
   a.src = d_src;
   a.src_size = P->info.src_bytes;
@@ -921,6 +925,10 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_jseg = (uint32_t)P->jsegd.size();
   a.j_rounds = P->j_rounds;
   a.j_pieces = P->j_pieces;
+  // hops per pending word and K4J round (c3s, scripts/exp_jhops.sh: 1 hop
+  // 10.2 ms, 2 5.2, 4 3.0, 8 2.44, 16 2.67, 32 2.95); ZD_J_HOPS overrides
+  static const char* hops_env = getenv("ZD_J_HOPS");
+  a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 8u;
   a.stream = s;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only

@@ -2282,14 +2282,17 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 //                     the period of an overlapping match, as the reference's
 //                     byte-by-byte push)
 //   KJ4 zd_k_jround   pointer jumping, in place: S[p] = S[S[p]] for every
-//                     pending word (a final source hands over its byte, a
-//                     pending one its pointer), so round r resolves chains of
-//                     up to 2^r - 1 hops.  A chain ends at a literal after at
-//                     most one hop per earlier match: ceil(log2(matches + 1))
-//                     rounds finish (launched with an early exit once nothing
-//                     is pending).  Any version of a word is true of its byte,
-//                     so lanes need no ordering within a round.
-//   KJ5 zd_k_jemit    the bytes of the state words -> the output
+//                     pending word, up to 8 hops per word and round (a final
+//                     source hands over its byte, a pending one its pointer).
+//                     A chain ends at a literal after at most one hop per
+//                     earlier match, and every hop of a round follows pointers
+//                     earlier rounds have already shortened: a 100 MB text
+//                     frame resolves in 2-3 rounds (the rounds launched for
+//                     the deepest possible chain exit at once once nothing is
+//                     pending).  Any version of a word is true of its byte,
+//                     so lanes need no ordering within a round.  A piece of
+//                     16 words is written to the output in the round that
+//                     resolves its last word.
 // ---------------------------------------------------------------------------
 __device__ inline bool j_live(uint64_t key, uint32_t j) {
   // a parse error ends the frame before any block decodes (frame.rs:198-230);
@@ -2744,33 +2747,37 @@ __device__ inline uint32_t j_frame_of(const JFrame* __restrict__ jframes, uint32
   return lo;
 }
 
-// One pointer-jumping round over the K4J frames' state words, 16 per thread:
-// S[p] = S[S[p]] for each pending word.  A piece inside one match whose
-// source run is contiguous reads it with four 16-byte loads; otherwise one
-// gather per pending word.
-__global__ __launch_bounds__(256) void zd_k_jround(FrameState* fstate, const JFrame* __restrict__ jframes,
-                                                   uint32_t n_jframes, uint64_t n_pieces, uint32_t* jst,
-                                                   uint32_t* pend, uint32_t r, uint32_t last) {
-  if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
-  uint32_t mine = 0;
-  for (uint64_t pc = (uint64_t)blockIdx.x * 256 + threadIdx.x; pc < n_pieces; pc += (uint64_t)gridDim.x * 256) {
-    const JFrame JF = jframes[j_frame_of(jframes, n_jframes, pc)];
-    const FrameState* S = &fstate[JF.frame];
-    if (S->key != KEY_NONE) continue;
-    const uint64_t total = S->out_len;
-    const uint64_t p0 = 16 * (pc - JF.piece0);
-    if (p0 >= total) continue;
-    const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
-    uint32_t* st = jst + JF.base;
-    uint32_t w[16];
-    j_load_words(st + p0, w);
-    uint32_t pm = 0, contig = 1;
+// One piece (16 state words) in a pointer-jumping round: S[p] = S[S[p]] for
+// each pending word, repeated up to `hops` times while some word of the
+// piece is still pending (every version of a word is true of its byte, so
+// more hops per round only shorten the chains faster).  A piece inside one
+// match whose source run is contiguous reads it with four 16-byte loads;
+// otherwise one gather per pending word.  A piece whose words are all final
+// is emitted -- its bytes to the frame's output -- and marked done, so later
+// rounds skip it without touching its words.  Returns true when the piece is
+// still pending.
+__device__ inline bool j_piece(uint8_t* outbase, const FrameDesc* __restrict__ frames, FrameState* fstate,
+                               const JFrame* __restrict__ jframes, uint32_t n_jframes, uint32_t* jst, uint8_t* done,
+                               uint64_t pc, uint32_t hops, uint32_t last) {
+  if (done[pc]) return false;
+  const JFrame JF = jframes[j_frame_of(jframes, n_jframes, pc)];
+  const FrameState* S = &fstate[JF.frame];
+  if (S->key != KEY_NONE) return false;
+  const uint64_t total = S->out_len;
+  const uint64_t p0 = 16 * (pc - JF.piece0);
+  if (p0 >= total) return false;
+  const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
+  uint32_t* st = jst + JF.base;
+  uint32_t w[16];
+  j_load_words(st + p0, w);
+  bool changed = false;
+  uint32_t pm = 0;
 #pragma unroll
-    for (uint32_t b = 0; b < 16; b++) {
-      pm |= (b < nb && !(w[b] & J_FINAL)) ? (1u << b) : 0u;
-      contig &= (uint32_t)(w[b] == w[0] + b);
-    }
-    if (!pm) continue;
+  for (uint32_t b = 0; b < 16; b++) pm |= (b < nb && !(w[b] & J_FINAL)) ? (1u << b) : 0u;
+  for (uint32_t h = 0; h < hops && pm; h++) {
+    uint32_t contig = 1;
+#pragma unroll
+    for (uint32_t b = 0; b < 16; b++) contig &= (uint32_t)(w[b] == w[0] + b);
     if (pm == 0xFFFFu && contig && w[0] + 16 <= total) {
       j_load_words(st + w[0], w);                  // one contiguous source run
     } else {
@@ -2780,40 +2787,46 @@ __global__ __launch_bounds__(256) void zd_k_jround(FrameState* fstate, const JFr
 #pragma unroll
       for (uint32_t b = 0; b < 16; b++) w[b] = v[b];
     }
-    uint32_t still = 0;
+    changed = true;
+    pm = 0;
 #pragma unroll
-    for (uint32_t b = 0; b < 16; b++) still |= (b < nb && !(w[b] & J_FINAL)) ? 1u : 0u;
-    j_store_words(st + p0, w, nb);
-    if (still) {
-      mine++;
-      if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
-    }
+    for (uint32_t b = 0; b < 16; b++) pm |= (b < nb && !(w[b] & J_FINAL)) ? (1u << b) : 0u;
   }
-  const uint64_t bm = __ballot(mine != 0);
-  if ((threadIdx.x & 63) == 0 && bm) atomicAdd(&pend[r], (uint32_t)__popcll(bm));
+  if (changed) j_store_words(st + p0, w, nb);
+  if (pm) {
+    if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
+    return true;
+  }
+  u32x4 v = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t b = 0; b < 16; b++) v[b >> 2] |= (w[b] & 255) << (8 * (b & 3));
+  j_store16(outbase + frames[JF.frame].out + p0, v, nb);
+  done[pc] = 1;
+  return false;
 }
 
-// The frames' bytes from their state words, 16 per thread (frames without a
-// failure only).
-__global__ __launch_bounds__(256) void zd_k_jemit(uint8_t* outbase, const FrameDesc* __restrict__ frames,
-                                                  const FrameState* __restrict__ fstate,
-                                                  const JFrame* __restrict__ jframes, uint32_t n_jframes,
-                                                  uint64_t n_pieces, const uint32_t* __restrict__ jst) {
-  for (uint64_t pc = (uint64_t)blockIdx.x * 256 + threadIdx.x; pc < n_pieces; pc += (uint64_t)gridDim.x * 256) {
-    const JFrame JF = jframes[j_frame_of(jframes, n_jframes, pc)];
-    const FrameState* S = &fstate[JF.frame];
-    if (S->key != KEY_NONE) continue;
-    const uint64_t total = S->out_len;
-    const uint64_t p0 = 16 * (pc - JF.piece0);
-    if (p0 >= total) continue;
-    const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
-    uint32_t w[16];
-    j_load_words(jst + JF.base + p0, w);
-    u32x4 v = (u32x4){0u, 0u, 0u, 0u};
-#pragma unroll
-    for (uint32_t b = 0; b < 16; b++) v[b >> 2] |= (w[b] & 255) << (8 * (b & 3));
-    j_store16(outbase + frames[JF.frame].out + p0, v, nb);
+// Pointer-jumping round r over the K4J frames' pieces (16 state words each).
+// Each XCD sweeps one contiguous eighth of the pieces in ascending order
+// (workgroups b and b + 8 share an XCD, speed only): match sources lie at
+// most a window behind, so they were updated earlier in the same round more
+// often and sit in that XCD's L2.  pend[r] counts the waves that left a
+// piece pending; a round after one that left none exits at once, so the
+// rounds launched for the deepest possible chain cost a launch each.
+__global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const FrameDesc* __restrict__ frames,
+                                                   FrameState* fstate, const JFrame* __restrict__ jframes,
+                                                   uint32_t n_jframes, uint64_t n_pieces, uint32_t* jst,
+                                                   uint32_t* pend, uint8_t* done, uint32_t hops, uint32_t r,
+                                                   uint32_t last) {
+  if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
+  const uint32_t x = blockIdx.x & 7, nk = gridDim.x >> 3;
+  const uint64_t R = (n_pieces + 7) / 8;
+  bool mine = false;
+  for (uint64_t i = (uint64_t)(blockIdx.x >> 3) * 256 + threadIdx.x; i < R; i += (uint64_t)nk * 256) {
+    const uint64_t pc = x * R + i;
+    if (pc < n_pieces) mine |= j_piece(outbase, frames, fstate, jframes, n_jframes, jst, done, pc, hops, last);
   }
+  const uint64_t bm = __ballot(mine);
+  if ((threadIdx.x & 63) == 0 && bm) atomicAdd(&pend[r], 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -2991,12 +3004,10 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, (const JSeg*)jseg, jsd, jst);
     const uint64_t gw = (a.j_pieces + 255) / 256;
-    const dim3 gr((uint32_t)(gw < 8192 ? (gw ? gw : 1) : 8192));
+    const dim3 gr((uint32_t)(gw < 8192 ? (gw + 7) & ~7ull : 8192));   // a multiple of 8 (one eighth per XCD)
     for (uint32_t r = 1; r <= a.j_rounds; r++)
-      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, fstate, jframes, a.n_jframes, a.j_pieces, jst, pend, r,
-                         (uint32_t)(r == a.j_rounds));
-    hipLaunchKernelGGL(zd_k_jemit, gr, dim3(256), 0, s, a.out, frames, (const FrameState*)fstate, jframes,
-                       a.n_jframes, a.j_pieces, (const uint32_t*)jst);
+      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes, a.j_pieces,
+                         jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == a.j_rounds));
   }
   if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;
   return hipGetLastError();

@@ -25,6 +25,7 @@ struct LaunchArgs {
   uint32_t n_jframes = 0, n_jblk = 0, n_jseg = 0;   // K4J frames / their blocks / scatter segments
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
+  uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
