@@ -75,6 +75,11 @@ extern "C" {
 #define ZD_E_NOT_DECODED     (-96) /* frame skipped: an earlier frame failed (FrameIterator stops, frame.rs:94-99) */
 #define ZD_E_COMM            (-97) /* an RCCL call failed, or RCCL is not loadable */
 
+/* Device workspaces of destroyed plans are kept for reuse by later plans of
+ * the process (bounded by ZD_WS_CACHE_MB, default 32 GiB; 0 disables it).
+ * zd_trim_cache frees them (every device). */
+void zd_trim_cache(void);
+
 /* Human-readable name of a status code (static storage). */
 const char* zd_status_name(int status);
 int zd_abi_version(void);
@@ -164,6 +169,8 @@ typedef struct zd_plan_info {
  * ends the plan (its status is kept and reported by zd_plan_results). */
 int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out);
 int zd_plan_info_get(const zd_plan* plan, zd_plan_info* info);
+/* Waits for the work the plan launched, then returns its device workspace to
+ * the process cache (zd_trim_cache). */
 void zd_plan_destroy(zd_plan* plan);
 
 /* Bitstream readers fetch aligned 16-byte windows and may touch up to

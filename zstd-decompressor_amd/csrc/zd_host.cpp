@@ -14,6 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -63,11 +66,20 @@ struct HostBlock {
   CompBlock cb;
 };
 
+// A frame; its blocks are blocks[b0, b0 + nb) of the part that holds it.
 struct HostFrame {
   zd_frame_desc d;
-  std::vector<HostBlock> blocks;
+  uint32_t b0 = 0, nb = 0;
+  uint32_t ncomp = 0;         // compressed blocks
   uint64_t key = KEY_NONE;    // host-detected parse error (frame stops here)
   int status = 0;
+};
+
+// Frames indexed by one thread of the host walk: a contiguous run of the
+// input's frames and their blocks, stored flat.
+struct HostPart {
+  std::vector<HostFrame> frames;
+  std::vector<HostBlock> blocks;
 };
 
 // Literals section header + the host-visible parts of the section
@@ -218,14 +230,23 @@ int parse_header(Bytes& in, zd_frame_desc* f) {
   return 0;
 }
 
-// Walks one frame at in.  On error, hf->key/status hold the failure; blocks
-// parsed before (and the failing one, with its host_stage) are kept.
-int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf) {
+// Walks one frame at in, appending its blocks to `blocks`.  On error,
+// hf->key/status hold the failure; blocks parsed before (and the failing one,
+// with its host_stage) are kept.
+int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf, std::vector<HostBlock>& blocks) {
   zd_frame_desc& f = hf->d;
   memset(&f, 0, sizeof f);
   f.src_offset = (uint64_t)(in.p - base);
   f.content_size = UINT64_MAX;
   f.dict_id = UINT64_MAX;
+  hf->b0 = (uint32_t)blocks.size();
+  hf->nb = 0;
+  hf->ncomp = 0;
+  auto push = [&](const HostBlock& hb) {
+    blocks.push_back(hb);
+    hf->nb++;
+    hf->ncomp += hb.type == 2;
+  };
   auto fail = [&](int code, uint32_t blk, uint32_t stage) {
     hf->status = code;
     hf->key = make_key(PH_PARSE, blk, stage, 0, code);
@@ -249,6 +270,9 @@ int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf) {
       hb.type = (x >> 1) & 3;
       hb.size = x >> 3;
       hb.src = (uint64_t)(in.p - base);
+      // the next block (or frame) header: a cache miss that now overlaps
+      // this block's own header parse
+      if (hb.type != 1 && hb.size < in.n) __builtin_prefetch(in.p + hb.size);
       if (hb.type == 0) {
         const uint8_t* s;
         if (int r = in.slice(hb.size, &s)) return fail(r, bi, PS_STRUCT);
@@ -266,18 +290,18 @@ int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf) {
         int r = parse_compressed(base, hb.src, hb.size, &cb, &e);
         if (r) {
           cb.host_stage = (uint8_t)e.stage;
-          hf->blocks.push_back(hb);
+          push(hb);
           return fail(r, bi, e.stage);
         }
       } else {
         return fail(ZD_E_RESERVED_BLOCK_TYPE, bi, PS_STRUCT);
       }
-      hf->blocks.push_back(hb);
+      push(hb);
       if (hb.last) break;
     }
     if (f.has_checksum) {
       uint64_t cs;
-      if (in.le(4, &cs)) return fail(ZD_E_MISSING_CHECKSUM, (uint32_t)hf->blocks.size(), PS_STRUCT);
+      if (in.le(4, &cs)) return fail(ZD_E_MISSING_CHECKSUM, hf->nb, PS_STRUCT);
       f.checksum = (uint32_t)cs;
     }
   } else if ((f.magic ^ MAGIC_SKIP) <= 0x0F) {
@@ -292,7 +316,7 @@ int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf) {
     hb.type = 4;
     hb.size = (uint32_t)len;
     hb.last = 1;
-    hf->blocks.push_back(hb);
+    push(hb);
   } else {
     return fail(ZD_E_UNRECOGNIZED_MAGIC, 0, PS_STRUCT);
   }
@@ -310,7 +334,9 @@ int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf) {
 // ===========================================================================
 struct zd_plan {
   uint32_t flags = 0;
-  std::vector<HostFrame> frames;
+  std::vector<HostPart> parts;          // the host walk's frames, in input order
+  std::vector<size_t> part_f0;          // plan frame index of each part's first frame
+  size_t nframes = 0;
   std::vector<CompBlock> comps;
   std::vector<BlockRec> blocks;
   std::vector<FrameDesc> fdesc;
@@ -322,18 +348,37 @@ struct zd_plan {
   std::vector<JSegDesc> jsegd;
   uint64_t j_bytes = 0, j_pieces = 0;
   uint32_t j_rounds = 0;
-  std::vector<uint64_t> frame_cap_off;   // output offset per frame (capacity layout)
+  // counts of the descriptor arrays (large plans keep their descriptors only
+  // in the pinned staging until the upload: the vectors above stay empty)
+  uint64_t n_comps = 0, n_blocks = 0, n_frames = 0, n_tables = 0, n_huf = 0, n_seq = 0, n_k4f = 0, n_copies = 0;
+  uint64_t n_jframes = 0, n_jblk = 0, n_jseg = 0;
+  std::vector<uint64_t> frame_out, frame_cap;   // output offset and capacity per frame
+  bool staged = false;
+  std::unique_lock<std::mutex> stage_lock;      // the pinned staging, from build_plan to upload_plan
   zd_plan_info info{};
   Workspace W{};
   uint8_t* d_ws = nullptr;
+  uint64_t ws_bytes = 0;                 // size of the d_ws allocation (>= W.total: a cached block)
+  uint64_t desc_bytes = 0;               // the host-filled head of the workspace (one upload)
   uint8_t* d_staging = nullptr;          // when the output layout is not exact
   uint64_t staging_bytes = 0;
   int index_status = 0;
-  size_t index_stop = 0;                 // frame index that failed to index (== frames.size()-1) or frames.size()
+  size_t index_stop = 0;                 // frame index that failed to index (== nframes - 1) or nframes
+  const HostFrame& frame(size_t f) const {
+    const size_t k = (size_t)(std::upper_bound(part_f0.begin(), part_f0.end(), f) - part_f0.begin()) - 1;
+    return parts[k].frames[f - part_f0[k]];
+  }
+  void set_parts(std::vector<HostPart>&& p) {
+    parts = std::move(p);
+    part_f0.clear();
+    nframes = 0;
+    for (const HostPart& hp : parts) { part_f0.push_back(nframes); nframes += hp.frames.size(); }
+  }
   bool profile = false;
   hipEvent_t ev[N_KERNELS + 1] = {};
   bool ev_made = false;
   bool launched = false;
+  hipStream_t last_stream = nullptr;     // the stream of the last zd_decode_async
   // context API hook: comp 0 is a prebuilt "previous block" carrying tables
   bool has_prebuilt = false;
   // second stream for K2 beside K3 (created on first launch)
@@ -362,248 +407,486 @@ constexpr uint32_t K4J_MIN_BLOCKS = 16;
 constexpr size_t K4J_MAX_FRAMES = 1024;
 constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
 
-// Builds device-side descriptors from the host frames.  `prev_*` seed the
-// Treeless/Repeat resolution (context API), -1 when absent.
-int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
-               const uint64_t rep0[3], uint64_t fixed_cap) {
-  uint64_t lits = 0, nseq_total = 0, nrec = 0, out_off = 0;
-  uint32_t lut_slots = 0, fse_slots = 0;
+// Running indices of build_plan: every array it fills grows frame by frame,
+// so a frame's entries start at the counts of the frames before it.
+struct PlanCounts {
+  uint64_t frames = 0, blocks = 0, comps = 0, luts = 0, fses = 0, lits = 0, nrec = 0, nseq = 0, out = 0;
+  uint64_t tables = 0, huf = 0, seq = 0, k4f = 0, copies = 0;
+  uint64_t jframes = 0, jblk = 0, jseg = 0;
   bool exact = true;
-  P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
-  P->frame_cap_off.clear(); P->jframes.clear(); P->jblkd.clear(); P->jsegd.clear();
-  static const char* k4f_env = getenv("ZD_K4F");
-  const bool k4f_on = k4f_env ? atoi(k4f_env) == 1
-                              : P->frames.size() >= K4F_AUTO_MIN_FRAMES && P->frames.size() <= K4F_AUTO_MAX_FRAMES;
-  static const char* k4j_env = getenv("ZD_K4J");
-  const int k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0
-                       : (k4j_env ? atoi(k4j_env) : -1);
-  auto ncomp_of = [](const HostFrame& hf) {
-    uint32_t c = 0;
-    for (const HostBlock& hb : hf.blocks) c += hb.type == 2;
-    return c;
-  };
-  size_t j_candidates = 0;
-  if (k4j_mode < 0 && out_len0 == 0)
-    for (const HostFrame& hf : P->frames) j_candidates += hf.key == KEY_NONE && ncomp_of(hf) >= K4J_MIN_BLOCKS;
-  const bool k4j_auto = j_candidates > 0 && j_candidates <= K4J_MAX_FRAMES;
-  uint64_t j_base = 0, j_pieces = 0, j_maxseq = 0;
-  for (size_t fi = 0; fi < P->frames.size(); fi++) {
-    HostFrame& hf = P->frames[fi];
-    FrameDesc fd{};
-    FrameState fs{};
-    fs.key = hf.key;
-    fs.rep[0] = rep0[0]; fs.rep[1] = rep0[1]; fs.rep[2] = rep0[2];
-    fd.first_block = (uint32_t)P->blocks.size();
-    fd.out_len0 = out_len0;
-    int32_t huf_prev = prev_huf;
-    int32_t tab_prev[3] = {prev_tab[0], prev_tab[1], prev_tab[2]};
-    uint64_t bound = 0;
-    bool seqs_in_frame = false;
-    bool frame_failed_host = hf.key != KEY_NONE;
-    for (size_t bi = 0; bi < hf.blocks.size(); bi++) {
-      HostBlock& hb = hf.blocks[bi];
-      BlockRec br{};
-      br.src = hb.src; br.size = hb.size; br.type = hb.type; br.last = hb.last; br.rle = hb.rle; br.comp = -1;
-      if (hb.type == 2) {
-        CompBlock cb = hb.cb;
-        cb.frame = (uint32_t)fi;
-        cb.block_in_frame = (uint32_t)bi;
-        cb.prebuilt = 0;
-        cb.huf_src = -1;
-        cb.tab_src[0] = cb.tab_src[1] = cb.tab_src[2] = -1;
-        uint32_t ci = (uint32_t)P->comps.size();
-        bool failing = cb.host_stage != PS_ALL;
-        // literals: Treeless resolution (literals.rs:59-66)
-        if (!failing && (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS)) {
-          if (cb.lit_type == LIT_COMPRESSED) { cb.huf_src = (int32_t)ci; huf_prev = (int32_t)ci; }
-          else cb.huf_src = huf_prev;
-          if (cb.huf_src < 0)
-            fs.key = std::min(fs.key, make_key(PH_DECODE, (uint32_t)bi, DS_LITERALS, 0, ZD_E_HUFFMAN_DECODER_MISSING));
-        }
-        if (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) cb.lut_slot = lut_slots++;
-        // sequences: Repeat resolution (sequences.rs:147-187, 232-234)
-        if (!failing) {
-          if (cb.nseq == 0) {
-            int code = ZD_E_EMPTY_INPUT_DATA;
-            for (int k = 0; k < 3; k++) if (tab_prev[k] < 0) { code = ZD_E_NO_PREVIOUS_DECODER; break; }
-            fs.key = std::min(fs.key, make_key(PH_DECODE, (uint32_t)bi, DS_SEQUENCES, 0, code));
-          } else {
-            cb.fse_slot = fse_slots++;
-            bool miss = false;
-            for (int k = 0; k < 3; k++) {
-              if (cb.modes[k] == M_REPEAT) {
-                if (tab_prev[k] < 0) { miss = true; break; }
-                cb.tab_src[k] = tab_prev[k];
-              } else {
-                cb.tab_src[k] = (int32_t)ci;
-              }
-            }
-            if (miss) fs.key = std::min(fs.key, make_key(PH_DECODE, (uint32_t)bi, DS_SEQUENCES, 0, ZD_E_NO_PREVIOUS_DECODER));
-            else for (int k = 0; k < 3; k++) tab_prev[k] = cb.tab_src[k];
-          }
-        } else if (cb.nseq) {
-          cb.fse_slot = fse_slots++;
-        }
-        // workspace
-        if (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) {
-          cb.lit_out = lits;
-          lits += align_up((uint64_t)cb.lit_regen + 16, 16);
-        }
-        cb.seq_out = nrec;
-        nseq_total += cb.nseq;
-        nrec += cb.nseq + (cb.nseq ? 2 : 0);     // K3 writes up to two spare records past the block's last
-        seqs_in_frame |= cb.nseq > 0;
-        P->comps.push_back(cb);
-        br.comp = (int32_t)ci;
-        bool needs_tables = (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) ||
-                            (cb.nseq > 0 && cb.host_stage > PS_SEQ_TABLES);
-        if (needs_tables) P->list_tables.push_back(ci);
-        if (!frame_failed_host) {
-          if ((cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) && cb.nstreams && cb.huf_src >= 0)
-            P->list_huf.push_back(ci);
-          if (cb.nseq > 0 && cb.tab_src[0] >= 0 && cb.tab_src[1] >= 0 && cb.tab_src[2] >= 0)
-            P->list_seq.push_back(ci);
-        }
-        bound += MAX_BLOCK_OUT;
-      } else {
-        bound += hb.size;
+  void add(const PlanCounts& o) {
+    frames += o.frames; blocks += o.blocks; comps += o.comps; luts += o.luts; fses += o.fses; lits += o.lits;
+    nrec += o.nrec; nseq += o.nseq; out += o.out; tables += o.tables; huf += o.huf; seq += o.seq; k4f += o.k4f;
+    copies += o.copies; jframes += o.jframes; jblk += o.jblk; jseg += o.jseg; exact = exact && o.exact;
+  }
+};
+
+// Plan-wide inputs of the per-frame pass.  `prev_*` seed the Treeless/Repeat
+// resolution (context API), -1 when absent.
+struct PlanCtx {
+  int32_t prev_huf;
+  int32_t prev_tab[3];
+  uint64_t out_len0, fixed_cap;
+  uint64_t rep0[3];
+  uint32_t flags;
+  bool k4f_on, k4j_auto;
+  int k4j_mode;
+};
+
+// Where the filling pass writes: the plan's host vectors (small plans, the
+// context API) or the pinned upload staging at the workspace offsets.
+struct Sink {
+  CompBlock* comps;
+  BlockRec* blocks;
+  FrameDesc* fdesc;
+  FrameState* fstate0;
+  uint32_t *list_tables, *list_huf, *list_seq, *list_k4f;
+  CopyDesc* copies;
+  JFrame* jframes;
+  JBlkDesc* jblkd;
+  JSegDesc* jsegd;
+  uint64_t *frame_out, *frame_cap;
+};
+
+// One frame's descriptors at the running indices c (build_plan).  FILL: the
+// entries are written to S; otherwise c only advances (the counting pass).
+// Frames for K4J are listed in *jfr (their descriptors come after, in order).
+template <bool FILL>
+void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks, PlanCounts& c, const Sink& S,
+                std::vector<uint32_t>* jfr) {
+  const uint32_t fi = (uint32_t)c.frames;
+  FrameDesc fd{};
+  FrameState fs{};
+  fs.key = hf.key;
+  fs.rep[0] = X.rep0[0]; fs.rep[1] = X.rep0[1]; fs.rep[2] = X.rep0[2];
+  fd.first_block = (uint32_t)c.blocks;
+  fd.out_len0 = X.out_len0;
+  int32_t huf_prev = X.prev_huf;
+  int32_t tab_prev[3] = {X.prev_tab[0], X.prev_tab[1], X.prev_tab[2]};
+  uint64_t bound = 0;
+  bool seqs_in_frame = false;
+  const bool frame_failed_host = hf.key != KEY_NONE;
+  uint64_t jseg = 0;
+  for (uint32_t bi = 0; bi < hf.nb; bi++) {
+    const HostBlock& hb = hblocks[hf.b0 + bi];
+    BlockRec br{};
+    br.src = hb.src; br.size = hb.size; br.type = hb.type; br.last = hb.last; br.rle = hb.rle; br.comp = -1;
+    if (hb.type == 2) {
+      CompBlock cb = hb.cb;
+      cb.frame = fi;
+      cb.block_in_frame = bi;
+      cb.prebuilt = 0;
+      cb.huf_src = -1;
+      cb.tab_src[0] = cb.tab_src[1] = cb.tab_src[2] = -1;
+      const uint32_t ci = (uint32_t)c.comps;
+      const bool failing = cb.host_stage != PS_ALL;
+      // literals: Treeless resolution (literals.rs:59-66)
+      if (!failing && (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS)) {
+        if (cb.lit_type == LIT_COMPRESSED) { cb.huf_src = (int32_t)ci; huf_prev = (int32_t)ci; }
+        else cb.huf_src = huf_prev;
+        if (cb.huf_src < 0)
+          fs.key = std::min(fs.key, make_key(PH_DECODE, bi, DS_LITERALS, 0, ZD_E_HUFFMAN_DECODER_MISSING));
       }
-      P->blocks.push_back(br);
-    }
-    fd.nblocks = (uint32_t)hf.blocks.size();
-    uint64_t cap;
-    if (hf.d.kind == ZD_FRAME_SKIPPABLE) {
-      // a truncated skippable frame fails to index and keeps no payload block
-      cap = ((P->flags & ZD_F_SKIPPABLE) && !hf.blocks.empty()) ? hf.blocks[0].size : 0;
-      if (!(P->flags & ZD_F_SKIPPABLE)) fd.nblocks = 0;
-    } else if (hf.d.content_size != UINT64_MAX && hf.d.content_size <= bound) {
-      cap = hf.d.content_size;
+      if (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) cb.lut_slot = (uint32_t)c.luts++;
+      // sequences: Repeat resolution (sequences.rs:147-187, 232-234)
+      if (!failing) {
+        if (cb.nseq == 0) {
+          int code = ZD_E_EMPTY_INPUT_DATA;
+          for (int k = 0; k < 3; k++) if (tab_prev[k] < 0) { code = ZD_E_NO_PREVIOUS_DECODER; break; }
+          fs.key = std::min(fs.key, make_key(PH_DECODE, bi, DS_SEQUENCES, 0, code));
+        } else {
+          cb.fse_slot = (uint32_t)c.fses++;
+          bool miss = false;
+          for (int k = 0; k < 3; k++) {
+            if (cb.modes[k] == M_REPEAT) {
+              if (tab_prev[k] < 0) { miss = true; break; }
+              cb.tab_src[k] = tab_prev[k];
+            } else {
+              cb.tab_src[k] = (int32_t)ci;
+            }
+          }
+          if (miss) fs.key = std::min(fs.key, make_key(PH_DECODE, bi, DS_SEQUENCES, 0, ZD_E_NO_PREVIOUS_DECODER));
+          else for (int k = 0; k < 3; k++) tab_prev[k] = cb.tab_src[k];
+        }
+      } else if (cb.nseq) {
+        cb.fse_slot = (uint32_t)c.fses++;
+      }
+      // workspace
+      if (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) {
+        cb.lit_out = c.lits;
+        c.lits += align_up((uint64_t)cb.lit_regen + 16, 16);
+      }
+      cb.seq_out = c.nrec;
+      c.nseq += cb.nseq;
+      c.nrec += cb.nseq + (cb.nseq ? 2 : 0);     // K3 writes up to two spare records past the block's last
+      seqs_in_frame |= cb.nseq > 0;
+      br.comp = (int32_t)ci;
+      jseg += cb.nseq > J_SEG ? (cb.nseq + J_SEG - 1) / J_SEG : 1;
+      const bool needs_tables = (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) ||
+                                (cb.nseq > 0 && cb.host_stage > PS_SEQ_TABLES);
+      if (needs_tables) { if (FILL) S.list_tables[c.tables] = ci; c.tables++; }
+      if (!frame_failed_host) {
+        if ((cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) && cb.nstreams && cb.huf_src >= 0) {
+          if (FILL) S.list_huf[c.huf] = ci;
+          c.huf++;
+        }
+        if (cb.nseq > 0 && cb.tab_src[0] >= 0 && cb.tab_src[1] >= 0 && cb.tab_src[2] >= 0) {
+          if (FILL) S.list_seq[c.seq] = ci;
+          c.seq++;
+        }
+      }
+      if (FILL) S.comps[ci] = cb;
+      c.comps++;
+      bound += MAX_BLOCK_OUT;
     } else {
-      cap = bound;
-      exact = false;
+      bound += hb.size;
+      jseg += 1;
     }
-    if (frame_failed_host) fd.nblocks = 0;
-    if (fixed_cap) cap = fixed_cap;
-    fd.out = out_off;
-    fd.out_cap = cap;
-    // K4J: frames of many compressed blocks (u32 positions)
-    const uint32_t ncomp = ncomp_of(hf);
-    const bool to_j = out_len0 == 0 && !frame_failed_host && fd.nblocks && ncomp && hf.d.kind == ZD_FRAME_ZSTD &&
-                      cap <= K4J_MAX_FRAME_OUT && (k4j_mode >= 0 ? k4j_mode == 1 : (k4j_auto && ncomp >= K4J_MIN_BLOCKS));
-    // the streaming K4 keeps int32 frame positions: larger frames with
-    // sequences that K4J does not take are outside the GPU path's domain
-    if (!to_j && cap > K4_MAX_FRAME_OUT && seqs_in_frame)
-      fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
-    if (to_j) {
-      fd.lds = 2;
+    if (FILL) S.blocks[c.blocks] = br;
+    c.blocks++;
+  }
+  fd.nblocks = hf.nb;
+  uint64_t cap;
+  if (hf.d.kind == ZD_FRAME_SKIPPABLE) {
+    // a truncated skippable frame fails to index and keeps no payload block
+    cap = ((X.flags & ZD_F_SKIPPABLE) && hf.nb) ? hblocks[hf.b0].size : 0;
+    if (!(X.flags & ZD_F_SKIPPABLE)) fd.nblocks = 0;
+  } else if (hf.d.content_size != UINT64_MAX && hf.d.content_size <= bound) {
+    cap = hf.d.content_size;
+  } else {
+    cap = bound;
+    c.exact = false;
+  }
+  if (frame_failed_host) fd.nblocks = 0;
+  if (X.fixed_cap) cap = X.fixed_cap;
+  fd.out = c.out;
+  fd.out_cap = cap;
+  // K4J: frames of many compressed blocks (u32 positions)
+  const bool to_j = X.out_len0 == 0 && !frame_failed_host && fd.nblocks && hf.ncomp && hf.d.kind == ZD_FRAME_ZSTD &&
+                    cap <= K4J_MAX_FRAME_OUT &&
+                    (X.k4j_mode >= 0 ? X.k4j_mode == 1 : (X.k4j_auto && hf.ncomp >= K4J_MIN_BLOCKS));
+  // the streaming K4 keeps int32 frame positions: larger frames with
+  // sequences that K4J does not take are outside the GPU path's domain
+  if (!to_j && cap > K4_MAX_FRAME_OUT && seqs_in_frame)
+    fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
+  if (to_j) {
+    fd.lds = 2;
+    c.jframes++;
+    c.jblk += fd.nblocks;
+    c.jseg += jseg;
+    if (FILL) jfr->push_back(fi);
+  } else {
+    // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
+    // executes the frames that fit it in plans of 256-768 frames, where the
+    // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
+    // it is slower on C4 (DESIGN.md §4).  ZD_K4F=1 / 0 forces it on / off.
+    fd.lds = (X.k4f_on && X.out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
+  }
+  if (fd.lds == 1) { if (FILL) S.list_k4f[c.k4f] = fi; c.k4f++; }
+  // Leading raw / RLE blocks (skippable payloads too) have output offsets
+  // known here: K0 copies them in parallel pieces, the streaming K4 starts
+  // after them (a frame of raw/RLE blocks only never reaches K4's loop).
+  if (!fd.lds && fd.nblocks && cap < 0x7FF00000ull) {
+    uint64_t pre = 0;
+    uint32_t k = 0;
+    for (; k < fd.nblocks; k++) {
+      const HostBlock& hb = hblocks[hf.b0 + k];
+      if (hb.type != 0 && hb.type != 1 && hb.type != 4) break;
+      if (X.out_len0 + pre + hb.size > cap) break;
+      for (uint64_t x = 0; x < hb.size; x += COPY_PIECE) {
+        if (FILL) {
+          CopyDesc cd{};
+          cd.src = hb.src + (hb.type == 1 ? 0 : x);
+          cd.dst = c.out + X.out_len0 + pre + x;
+          cd.size = (uint32_t)std::min<uint64_t>(COPY_PIECE, hb.size - x);
+          cd.fill = hb.type == 1 ? (0x100u | hb.rle) : 0u;
+          S.copies[c.copies] = cd;
+        }
+        c.copies++;
+      }
+      pre += hb.size;
+    }
+    fd.skip = k;
+    fd.skip_bytes = pre;
+  }
+  if (FILL) {
+    S.frame_out[fi] = c.out;
+    S.frame_cap[fi] = cap;
+    S.fdesc[fi] = fd;
+    S.fstate0[fi] = fs;
+  }
+  c.out += cap;
+  c.frames++;
+}
+
+// A process-wide pool of host worker threads (created on first use, kept:
+// spawning 15 threads per planner pass cost ~0.3 ms each time).
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool* p = new WorkerPool();   // never destroyed: workers idle on the cv at exit
+    return *p;
+  }
+  // f(k) for k in [0, n): k = 0 on the calling thread, the rest on the
+  // workers (n - 1 <= size()); returns when all ran.  Not reentrant from f.
+  void run(size_t n, const std::function<void(size_t)>& f) {
+    std::unique_lock<std::mutex> lk(m_);
+    while (busy_) idle_.wait(lk);              // one job at a time
+    busy_ = true;
+    job_ = &f;
+    next_ = 1;
+    end_ = n;
+    left_ = n - 1;
+    gen_++;
+    go_.notify_all();
+    lk.unlock();
+    f(0);
+    lk.lock();
+    done_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+    busy_ = false;
+    idle_.notify_one();
+  }
+  size_t size() const { return th_.size(); }
+
+ private:
+  WorkerPool() {
+    const unsigned n = std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1;
+    for (unsigned i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
+    for (auto& t : th_) t.detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      go_.wait(lk, [&] { return gen_ != seen && job_ && next_ < end_; });
+      seen = gen_;
+      while (job_ && next_ < end_) {
+        const size_t k = next_++;
+        const std::function<void(size_t)>* f = job_;
+        lk.unlock();
+        (*f)(k);
+        lk.lock();
+        if (--left_ == 0) done_.notify_all();
+      }
+    }
+  }
+  std::mutex m_;
+  std::condition_variable go_, done_, idle_;
+  std::vector<std::thread> th_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  size_t next_ = 0, end_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool busy_ = false;
+};
+
+// Runs f(k) for k in [0, n) in parallel (the calling thread takes k = 0;
+// n - 1 must not exceed the pool's workers, else the rest run inline).
+template <typename F>
+void run_parts(size_t n, F f) {
+  if (n <= 1) { if (n) f(0); return; }
+  WorkerPool& pool = WorkerPool::get();
+  const size_t par = std::min(n, pool.size() + 1);
+  const std::function<void(size_t)> g = [&](size_t k) { for (size_t j = k; j < n; j += par) f(j); };
+  pool.run(par, g);
+}
+
+// Pinned host staging for the descriptor upload, kept between plans: large
+// plans write their descriptors straight into it at the workspace offsets
+// (pinned pages never fault) and upload them with one DMA.
+struct HostStage {
+  std::mutex m;
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  bool pinned = false;     // hipHostMalloc (else malloc: no device to pin for)
+  void release() {
+    if (p) { if (pinned) (void)hipHostFree(p); else free(p); }
+    p = nullptr;
+    cap = 0;
+  }
+};
+HostStage& host_stage() {
+  static HostStage h;
+  return h;
+}
+constexpr uint64_t STAGE_MIN_BYTES = 1u << 20;     // smaller plans fill host vectors
+
+// Builds device-side descriptors from the host frames: one counting pass and
+// one filling pass over the parts in parallel (each part's entries start at
+// the counts of the parts before it), then the K4J descriptors in frame order.
+// `staged`: a large plan may fill the pinned staging (zd_plan_create); the
+// context API keeps host vectors it edits afterwards.
+int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
+               const uint64_t rep0[3], uint64_t fixed_cap, bool staged = false) {
+  PlanCtx X{};
+  X.prev_huf = prev_huf;
+  for (int k = 0; k < 3; k++) { X.prev_tab[k] = prev_tab[k]; X.rep0[k] = rep0[k]; }
+  X.out_len0 = out_len0;
+  X.fixed_cap = fixed_cap;
+  X.flags = P->flags;
+  static const char* k4f_env = getenv("ZD_K4F");
+  X.k4f_on = k4f_env ? atoi(k4f_env) == 1 : P->nframes >= K4F_AUTO_MIN_FRAMES && P->nframes <= K4F_AUTO_MAX_FRAMES;
+  static const char* k4j_env = getenv("ZD_K4J");
+  X.k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0 : (k4j_env ? atoi(k4j_env) : -1);
+  size_t j_candidates = 0;
+  if (X.k4j_mode < 0 && out_len0 == 0)
+    for (const HostPart& hp : P->parts)
+      for (const HostFrame& hf : hp.frames) j_candidates += hf.key == KEY_NONE && hf.ncomp >= K4J_MIN_BLOCKS;
+  X.k4j_auto = j_candidates > 0 && j_candidates <= K4J_MAX_FRAMES;
+
+  const size_t np = P->parts.size();
+  std::vector<PlanCounts> cnt(np + 1);
+  const Sink none{};
+  run_parts(np, [&](size_t k) {
+    const HostPart& hp = P->parts[k];
+    PlanCounts c;
+    for (const HostFrame& hf : hp.frames) plan_frame<false>(X, hf, hp.blocks.data(), c, none, nullptr);
+    cnt[k + 1] = c;
+  });
+  for (size_t k = 1; k <= np; k++) { PlanCounts t = cnt[k - 1]; t.add(cnt[k]); cnt[k] = t; }
+  const PlanCounts T = cnt[np];
+
+  // workspace carve-up: the arrays the host fills first (one upload), then
+  // the device-only ones
+  Workspace& W = P->W;
+  uint64_t o = 0;
+  auto carve = [&](uint64_t bytes) { uint64_t r = o; o = align_up(o + bytes, 256); return r; };
+  W.comp = carve(sizeof(CompBlock) * std::max<uint64_t>(T.comps, 1));
+  W.blocks = carve(sizeof(BlockRec) * std::max<uint64_t>(T.blocks, 1));
+  W.frames = carve(sizeof(FrameDesc) * std::max<uint64_t>(T.frames, 1));
+  W.frame_state0 = carve(sizeof(FrameState) * std::max<uint64_t>(T.frames, 1));
+  W.list_tables = carve(4 * std::max<uint64_t>(T.tables, 1));
+  W.list_huf = carve(4 * std::max<uint64_t>(T.huf, 1));
+  W.list_seq = carve(4 * std::max<uint64_t>(T.seq, 1));
+  W.list_k4f = carve(4 * std::max<uint64_t>(T.k4f, 1));
+  W.copies = carve(sizeof(CopyDesc) * std::max<uint64_t>(T.copies, 1));
+  W.jframes = carve(sizeof(JFrame) * std::max<uint64_t>(T.jframes, 1));
+  W.jblkd = carve(sizeof(JBlkDesc) * std::max<uint64_t>(T.jblk, 1));
+  W.jsegd = carve(sizeof(JSegDesc) * std::max<uint64_t>(T.jseg, 1));
+  P->desc_bytes = o;
+
+  P->n_comps = T.comps; P->n_blocks = T.blocks; P->n_frames = T.frames;
+  P->n_tables = T.tables; P->n_huf = T.huf; P->n_seq = T.seq; P->n_k4f = T.k4f; P->n_copies = T.copies;
+  P->n_jframes = T.jframes; P->n_jblk = T.jblk; P->n_jseg = T.jseg;
+  P->frame_out.resize(T.frames);
+  P->frame_cap.resize(T.frames);
+  Sink S{};
+  P->staged = staged && P->desc_bytes >= STAGE_MIN_BYTES;
+  if (P->staged) {
+    // held until upload_plan has copied the staging out
+    P->stage_lock = std::unique_lock<std::mutex>(host_stage().m);
+    HostStage& H = host_stage();
+    if (H.cap < P->desc_bytes) {
+      H.release();
+      const size_t want = P->desc_bytes + (P->desc_bytes >> 2);
+      H.pinned = hipHostMalloc((void**)&H.p, want, hipHostMallocDefault) == hipSuccess;
+      if (!H.pinned) {
+        (void)hipGetLastError();
+        H.p = (uint8_t*)aligned_alloc(4096, align_up(want, 4096));
+      }
+      if (!H.p) return ZD_E_NO_MEMORY;
+      H.cap = want;
+    }
+    uint8_t* b = H.p;
+    S = Sink{(CompBlock*)(b + W.comp), (BlockRec*)(b + W.blocks), (FrameDesc*)(b + W.frames),
+             (FrameState*)(b + W.frame_state0), (uint32_t*)(b + W.list_tables), (uint32_t*)(b + W.list_huf),
+             (uint32_t*)(b + W.list_seq), (uint32_t*)(b + W.list_k4f), (CopyDesc*)(b + W.copies),
+             (JFrame*)(b + W.jframes), (JBlkDesc*)(b + W.jblkd), (JSegDesc*)(b + W.jsegd), nullptr, nullptr};
+    P->comps.clear(); P->blocks.clear(); P->fdesc.clear(); P->fstate0.clear();
+    P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
+    P->jframes.clear(); P->jblkd.clear(); P->jsegd.clear();
+  } else {
+    P->comps.assign(T.comps, CompBlock{});
+    P->blocks.assign(T.blocks, BlockRec{});
+    P->fdesc.assign(T.frames, FrameDesc{});
+    P->fstate0.assign(T.frames, FrameState{});
+    P->list_tables.assign(T.tables, 0);
+    P->list_huf.assign(T.huf, 0);
+    P->list_seq.assign(T.seq, 0);
+    P->list_k4f.assign(T.k4f, 0);
+    P->copies.assign(T.copies, CopyDesc{});
+    P->jframes.assign(T.jframes, JFrame{});
+    P->jblkd.assign(T.jblk, JBlkDesc{});
+    P->jsegd.assign(T.jseg, JSegDesc{});
+    S = Sink{P->comps.data(), P->blocks.data(), P->fdesc.data(), P->fstate0.data(), P->list_tables.data(),
+             P->list_huf.data(), P->list_seq.data(), P->list_k4f.data(), P->copies.data(), P->jframes.data(),
+             P->jblkd.data(), P->jsegd.data(), nullptr, nullptr};
+  }
+  S.frame_out = P->frame_out.data();
+  S.frame_cap = P->frame_cap.data();
+  std::vector<std::vector<uint32_t>> jfr(np);
+  run_parts(np, [&](size_t k) {
+    const HostPart& hp = P->parts[k];
+    PlanCounts c = cnt[k];
+    for (const HostFrame& hf : hp.frames) plan_frame<true>(X, hf, hp.blocks.data(), c, S, &jfr[k]);
+  });
+
+  // K4J descriptors, frames in order
+  uint64_t j_base = 0, j_pieces = 0, j_maxseq = 0;
+  uint32_t nj = 0, njb = 0, njs = 0;
+  for (const auto& part : jfr) {
+    for (uint32_t fi : part) {
+      const FrameDesc& fd = S.fdesc[fi];
       JFrame jf{};
       jf.base = align_up(j_base, 16);          // word index: frame pieces of 16 words are 64-byte lines
-      jf.cap = cap;
+      jf.cap = fd.out_cap;
       jf.piece0 = j_pieces;
-      jf.frame = (uint32_t)fi;
-      jf.jb0 = (uint32_t)P->jblkd.size();
+      jf.frame = fi;
+      jf.jb0 = njb;
       jf.njb = fd.nblocks;
       uint64_t nseq = 0;
       for (uint32_t k = 0; k < fd.nblocks; k++) {
         JBlkDesc d{};
         d.block = fd.first_block + k;
-        d.jframe = (uint32_t)P->jframes.size();
+        d.jframe = nj;
         d.j = k;
-        d.seg0 = (uint32_t)P->jsegd.size();
-        const BlockRec& br = P->blocks[fd.first_block + k];
-        const uint32_t bn = br.comp >= 0 ? P->comps[(size_t)br.comp].nseq : 0;
+        d.seg0 = njs;
+        const BlockRec& br = S.blocks[fd.first_block + k];
+        const uint32_t bn = br.comp >= 0 ? S.comps[(size_t)br.comp].nseq : 0;
         nseq += bn;
-        for (uint32_t g = 0; g == 0 || g * J_SEG < bn; g++) P->jsegd.push_back(JSegDesc{(uint32_t)P->jblkd.size(), g});
-        P->jblkd.push_back(d);
+        for (uint32_t g = 0; g == 0 || g * J_SEG < bn; g++) S.jsegd[njs++] = JSegDesc{njb, g};
+        S.jblkd[njb++] = d;
       }
       j_maxseq = std::max(j_maxseq, nseq);
-      j_base = jf.base + cap + 16;
-      j_pieces += (cap + 15) / 16;
-      P->jframes.push_back(jf);
+      j_base = jf.base + fd.out_cap + 16;
+      j_pieces += (fd.out_cap + 15) / 16;
+      S.jframes[nj++] = jf;
     }
-    // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
-    // executes the frames that fit it in plans of 256-768 frames, where the
-    // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
-    // it is slower on C4 (DESIGN.md §4).  ZD_K4F=1 / 0 forces it on / off.
-    if (!to_j) fd.lds = (k4f_on && out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
-    if (fd.lds == 1) P->list_k4f.push_back((uint32_t)fi);
-    // Leading raw / RLE blocks (skippable payloads too) have output offsets
-    // known here: K0 copies them in parallel pieces, the streaming K4 starts
-    // after them (a frame of raw/RLE blocks only never reaches K4's loop).
-    if (!fd.lds && fd.nblocks && cap < 0x7FF00000ull) {
-      uint64_t pre = 0;
-      uint32_t k = 0;
-      for (; k < fd.nblocks; k++) {
-        const BlockRec& br = P->blocks[fd.first_block + k];
-        if (br.type != 0 && br.type != 1 && br.type != 4) break;
-        if (out_len0 + pre + br.size > cap) break;
-        for (uint64_t x = 0; x < br.size; x += COPY_PIECE) {
-          CopyDesc c{};
-          c.src = br.src + (br.type == 1 ? 0 : x);
-          c.dst = out_off + out_len0 + pre + x;
-          c.size = (uint32_t)std::min<uint64_t>(COPY_PIECE, br.size - x);
-          c.fill = br.type == 1 ? (0x100u | br.rle) : 0u;
-          P->copies.push_back(c);
-        }
-        pre += br.size;
-      }
-      fd.skip = k;
-      fd.skip_bytes = pre;
-    }
-    P->frame_cap_off.push_back(out_off);
-    out_off += cap;
-    P->fdesc.push_back(fd);
-    P->fstate0.push_back(fs);
   }
-  // workspace carve-up
-  Workspace& W = P->W;
-  uint64_t o = 0;
-  auto carve = [&](uint64_t bytes) { uint64_t r = o; o = align_up(o + bytes, 256); return r; };
-  W.comp = carve(sizeof(CompBlock) * std::max<size_t>(P->comps.size(), 1));
-  W.comp_state = carve(sizeof(CompState) * std::max<size_t>(P->comps.size(), 1));
-  W.blocks = carve(sizeof(BlockRec) * std::max<size_t>(P->blocks.size(), 1));
-  W.frames = carve(sizeof(FrameDesc) * std::max<size_t>(P->fdesc.size(), 1));
-  W.frame_state = carve(sizeof(FrameState) * std::max<size_t>(P->fdesc.size(), 1));
-  W.frame_state0 = carve(sizeof(FrameState) * std::max<size_t>(P->fdesc.size(), 1));
-  W.list_tables = carve(4 * std::max<size_t>(P->list_tables.size(), 1));
-  W.list_huf = carve(4 * std::max<size_t>(P->list_huf.size(), 1));
-  W.list_seq = carve(4 * std::max<size_t>(P->list_seq.size(), 1));
-  W.list_k4f = carve(4 * std::max<size_t>(P->list_k4f.size(), 1));
-  W.copies = carve(sizeof(CopyDesc) * std::max<size_t>(P->copies.size(), 1));
-  W.lits = carve(lits + 64);
-  W.seqs = carve(8 * nrec + 64);
-  W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint32_t>(lut_slots, 1));
-  W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint32_t>(fse_slots, 1));
+
+  W.comp_state = carve(sizeof(CompState) * std::max<uint64_t>(T.comps, 1));
+  W.frame_state = carve(sizeof(FrameState) * std::max<uint64_t>(T.frames, 1));
+  W.lits = carve(T.lits + 64);
+  W.seqs = carve(8 * T.nrec + 64);
+  W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint64_t>(T.luts, 1));
+  W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint64_t>(T.fses, 1));
   // K4J: pointer jumping resolves every match byte within ceil(log2(matches
   // + 1)) rounds (each pointer chain ends at a literal after at most one hop
   // per earlier match; each round halves the hops left)
-  P->j_bytes = P->jframes.empty() ? 0 : j_base + 16;
+  P->j_bytes = T.jframes ? j_base + 16 : 0;
   P->j_pieces = j_pieces;
   P->j_rounds = 0;
-  if (!P->jframes.empty()) {
+  if (T.jframes) {
     uint32_t r = 1;
     while (r < (uint32_t)J_MAX_ROUNDS - 1 && (1ull << r) <= j_maxseq + 1) r++;
     P->j_rounds = r + 1;
   }
-  W.jframes = carve(sizeof(JFrame) * std::max<size_t>(P->jframes.size(), 1));
-  W.jblkd = carve(sizeof(JBlkDesc) * std::max<size_t>(P->jblkd.size(), 1));
-  W.jblk = carve(sizeof(JBlk) * std::max<size_t>(P->jblkd.size(), 1));
-  W.jseg = carve(sizeof(JSeg) * std::max<size_t>(P->jsegd.size(), 1));
-  W.jsegd = carve(sizeof(JSegDesc) * std::max<size_t>(P->jsegd.size(), 1));
+  W.jblk = carve(sizeof(JBlk) * std::max<uint64_t>(T.jblk, 1));
+  W.jseg = carve(sizeof(JSeg) * std::max<uint64_t>(T.jseg, 1));
   W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
   W.jdone = carve(std::max<uint64_t>(j_pieces, 1));
   W.jst = carve(4 * P->j_bytes + 64);
   W.total = o;
 
   zd_plan_info& I = P->info;
-  I.nframes = P->fdesc.size();
-  I.nblocks = P->blocks.size();
-  I.ncompressed = P->comps.size();
-  I.out_bytes = out_off;
-  I.out_exact = exact;
+  I.nframes = T.frames;
+  I.nblocks = T.blocks;
+  I.ncompressed = T.comps;
+  I.out_bytes = T.out;
+  I.out_exact = T.exact;
   I.workspace_bytes = W.total;
-  I.nsequences = nseq_total;
-  I.nliterals = lits;
+  I.nsequences = T.nseq;
+  I.nliterals = T.lits;
   I.index_status = P->index_status;
   return 0;
 }
@@ -614,24 +897,113 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
 constexpr size_t FORK_MAX_SEQ_BLOCKS = 2 * 256 * 16;
 constexpr size_t FORK_MIN_SEQ_BLOCKS = 256;
 
+// Device workspaces of destroyed plans, kept for the next plans of this
+// process (a plan's workspace is up to ~1.2x its decoded bytes: K3's
+// records, the literals, the tables).  A plan takes a cached block of at
+// least its size and at most 1.25x + 64 MiB; zd_trim_cache() frees them all,
+// and so does a failed allocation before its retry.  ZD_WS_CACHE_MB caps
+// the bytes held (default 32 GiB; 0 disables the cache).
+struct WsCache {
+  struct E { int dev; uint8_t* p; uint64_t bytes; };
+  std::mutex m;
+  std::vector<E> free;
+  uint64_t held = 0;
+};
+WsCache& ws_cache() {
+  static WsCache c;
+  return c;
+}
+uint64_t ws_cache_limit() {
+  static const uint64_t lim = getenv("ZD_WS_CACHE_MB") ? strtoull(getenv("ZD_WS_CACHE_MB"), nullptr, 0) << 20
+                                                       : 32ull << 30;
+  return lim;
+}
+void ws_trim(int dev) {           // dev < 0: every device
+  WsCache& C = ws_cache();
+  std::lock_guard<std::mutex> g(C.m);
+  for (size_t i = 0; i < C.free.size();) {
+    if (dev < 0 || C.free[i].dev == dev) {
+      (void)hipFree(C.free[i].p);
+      C.held -= C.free[i].bytes;
+      C.free.erase(C.free.begin() + (long)i);
+    } else {
+      i++;
+    }
+  }
+}
+hipError_t ws_alloc(uint64_t bytes, uint8_t** p, uint64_t* got) {
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  {
+    WsCache& C = ws_cache();
+    std::lock_guard<std::mutex> g(C.m);
+    size_t best = SIZE_MAX;
+    for (size_t i = 0; i < C.free.size(); i++) {
+      const WsCache::E& e = C.free[i];
+      if (e.dev == dev && e.bytes >= bytes && e.bytes <= bytes + bytes / 4 + (64ull << 20) &&
+          (best == SIZE_MAX || e.bytes < C.free[best].bytes))
+        best = i;
+    }
+    if (best != SIZE_MAX) {
+      *p = C.free[best].p;
+      *got = C.free[best].bytes;
+      C.held -= *got;
+      C.free.erase(C.free.begin() + (long)best);
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    ws_trim(dev);
+    e = hipMalloc(p, bytes);
+  }
+  *got = bytes;
+  return e;
+}
+void ws_release(uint8_t* p, uint64_t bytes) {
+  if (!p) return;
+  int dev = 0;
+  const uint64_t lim = ws_cache_limit();
+  if (hipGetDevice(&dev) != hipSuccess || bytes > lim) { (void)hipFree(p); return; }
+  WsCache& C = ws_cache();
+  std::lock_guard<std::mutex> g(C.m);
+  C.free.push_back(WsCache::E{dev, p, bytes});
+  C.held += bytes;
+  while (C.held > lim || C.free.size() > 4) {        // oldest first
+    (void)hipFree(C.free.front().p);
+    C.held -= C.free.front().bytes;
+    C.free.erase(C.free.begin());
+  }
+}
+
 int upload_plan(zd_plan* P) {
-  HIPCHK(hipMalloc(&P->d_ws, P->W.total));
-  auto up = [&](uint64_t off, const void* p, size_t bytes) -> int {
-    if (bytes) HIPCHK(hipMemcpy(P->d_ws + off, p, bytes, hipMemcpyHostToDevice));
-    return 0;
-  };
-  if (int r = up(P->W.comp, P->comps.data(), P->comps.size() * sizeof(CompBlock))) return r;
-  if (int r = up(P->W.blocks, P->blocks.data(), P->blocks.size() * sizeof(BlockRec))) return r;
-  if (int r = up(P->W.frames, P->fdesc.data(), P->fdesc.size() * sizeof(FrameDesc))) return r;
-  if (int r = up(P->W.list_tables, P->list_tables.data(), P->list_tables.size() * 4)) return r;
-  if (int r = up(P->W.list_huf, P->list_huf.data(), P->list_huf.size() * 4)) return r;
-  if (int r = up(P->W.list_seq, P->list_seq.data(), P->list_seq.size() * 4)) return r;
-  if (int r = up(P->W.list_k4f, P->list_k4f.data(), P->list_k4f.size() * 4)) return r;
-  if (int r = up(P->W.copies, P->copies.data(), P->copies.size() * sizeof(CopyDesc))) return r;
-  if (int r = up(P->W.frame_state0, P->fstate0.data(), P->fstate0.size() * sizeof(FrameState))) return r;
-  if (int r = up(P->W.jframes, P->jframes.data(), P->jframes.size() * sizeof(JFrame))) return r;
-  if (int r = up(P->W.jblkd, P->jblkd.data(), P->jblkd.size() * sizeof(JBlkDesc))) return r;
-  if (int r = up(P->W.jsegd, P->jsegd.data(), P->jsegd.size() * sizeof(JSegDesc))) return r;
+  HIPCHK(ws_alloc(P->W.total, &P->d_ws, &P->ws_bytes));
+  if (P->staged) {
+    // the descriptors are in the pinned staging at their workspace offsets
+    const hipError_t e = hipMemcpy(P->d_ws, host_stage().p, P->desc_bytes, hipMemcpyHostToDevice);
+    P->stage_lock = std::unique_lock<std::mutex>();
+    HIPCHK(e);
+  } else {
+    const Workspace& W = P->W;
+    struct Piece { uint64_t off; const void* p; size_t bytes; };
+    const Piece pieces[] = {
+        {W.comp, P->comps.data(), P->comps.size() * sizeof(CompBlock)},
+        {W.blocks, P->blocks.data(), P->blocks.size() * sizeof(BlockRec)},
+        {W.frames, P->fdesc.data(), P->fdesc.size() * sizeof(FrameDesc)},
+        {W.frame_state0, P->fstate0.data(), P->fstate0.size() * sizeof(FrameState)},
+        {W.list_tables, P->list_tables.data(), P->list_tables.size() * 4},
+        {W.list_huf, P->list_huf.data(), P->list_huf.size() * 4},
+        {W.list_seq, P->list_seq.data(), P->list_seq.size() * 4},
+        {W.list_k4f, P->list_k4f.data(), P->list_k4f.size() * 4},
+        {W.copies, P->copies.data(), P->copies.size() * sizeof(CopyDesc)},
+        {W.jframes, P->jframes.data(), P->jframes.size() * sizeof(JFrame)},
+        {W.jblkd, P->jblkd.data(), P->jblkd.size() * sizeof(JBlkDesc)},
+        {W.jsegd, P->jsegd.data(), P->jsegd.size() * sizeof(JSegDesc)},
+    };
+    for (const Piece& q : pieces)
+      if (q.bytes) HIPCHK(hipMemcpy(P->d_ws + q.off, q.p, q.bytes, hipMemcpyHostToDevice));
+  }
   if (!P->info.out_exact) {
     P->staging_bytes = P->info.out_bytes;
     HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
@@ -639,106 +1011,148 @@ int upload_plan(zd_plan* P) {
   return 0;
 }
 
-// One frame's extent from its headers alone (magic, frame header, block
-// headers, checksum), without parsing block contents.  false wherever
-// index_frame could fail or the structure is unusual (the walk hands the rest
-// to a serial index).
-bool skip_frame(Bytes& in) {
-  uint64_t magic;
-  if (in.le(4, &magic)) return false;
-  if ((uint32_t)magic == MAGIC_ZSTD) {
-    zd_frame_desc f;
-    memset(&f, 0, sizeof f);
-    if (parse_header(in, &f) || f.window_size > MAX_WIN_SIZE) return false;
-    for (;;) {
-      uint64_t x;
-      if (in.le(3, &x)) return false;
-      const uint32_t type = (x >> 1) & 3, size = (uint32_t)(x >> 3);
-      const uint64_t len = type == 1 ? 1 : size;
-      if (type == 3 || len == 0 || in.n < len) return false;
-      in.p += len; in.n -= len;
-      if (x & 1) break;
+// A plan's second stream and its fork/join events, kept for the next plans
+// of the process (creating them took ~0.25 ms per plan).
+struct AuxSet { int dev; hipStream_t s; hipEvent_t fork, join; };
+std::mutex& aux_mutex() {
+  static std::mutex m;
+  return m;
+}
+std::vector<AuxSet>& aux_free() {
+  static std::vector<AuxSet>* v = new std::vector<AuxSet>();   // never destroyed (no HIP calls at exit)
+  return *v;
+}
+bool aux_take(zd_plan* P) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  {
+    std::lock_guard<std::mutex> g(aux_mutex());
+    auto& v = aux_free();
+    for (size_t i = 0; i < v.size(); i++) {
+      if (v[i].dev != dev) continue;
+      P->aux = v[i].s; P->fork = v[i].fork; P->join = v[i].join;
+      v.erase(v.begin() + (long)i);
+      return true;
     }
-    if (f.has_checksum) {
-      if (in.n < 4) return false;
-      in.p += 4; in.n -= 4;
+  }
+  return hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&P->fork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&P->join, hipEventDisableTiming) == hipSuccess;
+}
+void aux_give(zd_plan* P) {
+  int dev = 0;
+  if (P->aux && P->fork && P->join && hipGetDevice(&dev) == hipSuccess) {
+    std::lock_guard<std::mutex> g(aux_mutex());
+    if (aux_free().size() < 8) {
+      aux_free().push_back(AuxSet{dev, P->aux, P->fork, P->join});
+      P->aux = nullptr; P->fork = P->join = nullptr;
+      return;
     }
-    return true;
   }
-  if (((uint32_t)magic ^ MAGIC_SKIP) <= 0x0F) {
-    uint64_t len;
-    if (in.le(4, &len) || len == 0 || in.n < len) return false;
-    in.p += len; in.n -= len;
-    return true;
-  }
-  return false;
+  if (P->fork) (void)hipEventDestroy(P->fork);
+  if (P->join) (void)hipEventDestroy(P->join);
+  if (P->aux) (void)hipStreamDestroy(P->aux);
+  P->aux = nullptr; P->fork = P->join = nullptr;
 }
 
-// Frames from in (FrameIterator::next, frame.rs:94-99) until the input ends,
-// `limit` frames are indexed, or one fails (kept, with its status).
-int index_frames(const uint8_t* src, Bytes& in, size_t limit, std::vector<HostFrame>& out) {
-  while (in.n && out.size() < limit) {
+// Frames from in (FrameIterator::next, frame.rs:94-99) into `part` until the
+// input ends, a frame starting at or past `stop` comes up, or one fails (kept,
+// with its status).
+int index_frames(const uint8_t* src, Bytes& in, size_t stop, HostPart& part) {
+  while (in.n && (size_t)(in.p - src) < stop) {
     HostFrame hf;
-    int r = index_frame(src, in, &hf);
-    out.push_back(std::move(hf));
+    int r = index_frame(src, in, &hf, part.blocks);
+    part.frames.push_back(hf);
     if (r) return r;
   }
   return 0;
 }
 
-// The host walk.  Large inputs: a serial header-only pass finds the frame
-// extents, then threads index contiguous frame ranges (the compressed-block
-// headers parsed in parallel); the result is the serial walk's, first failing
-// frame included -- a range that does not end where the next one starts
-// (cannot happen while skip_frame and index_frame agree) falls back to it.
+inline bool magic_at(const uint8_t* p) {
+  uint32_t m;
+  memcpy(&m, p, 4);
+  return m == MAGIC_ZSTD || (m ^ MAGIC_SKIP) <= 0x0F;
+}
+
+// The host walk (FrameIterator over the whole input).  Large inputs are cut
+// into T byte ranges; thread k finds the first frame magic in its range and
+// indexes the chain of frames from there while they start inside the range.
+// Each frame's start follows from the one before it, so a chain that reaches
+// a position of the true chain (the one from offset 0) is the true chain
+// from there on.  The stitch checks exactly that: range k's frames are kept
+// from the frame that starts where the kept frames before it end; a range
+// whose chain never meets that position (a magic number inside data, or a
+// frame longer than a range) is dropped and the walk continues serially.
+// The result is the serial walk's, first failing frame included.
 int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
-  std::vector<size_t> starts;
-  if (n >= PAR_INDEX_MIN_BYTES) {
-    Bytes w{src, n};
-    while (w.n) {
-      const size_t at = (size_t)(w.p - src);
-      if (!skip_frame(w)) break;
-      starts.push_back(at);
-    }
-  }
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const size_t T = std::min<size_t>(hw, starts.size() / 256);
-  if (T >= 2) {
-    std::vector<std::vector<HostFrame>> part(T);
-    std::vector<int> st(T, 0);
-    std::vector<size_t> end(T, 0);
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < T; k++) {
-      const size_t f0 = starts.size() * k / T, f1 = starts.size() * (k + 1) / T;
-      th.emplace_back([&, k, f0, f1] {
-        part[k].reserve(f1 - f0 + 1);
-        Bytes in{src + starts[f0], n - starts[f0]};
-        // the last range runs on past the skipped frames, to the input's end
-        st[k] = index_frames(src, in, k + 1 == T ? SIZE_MAX : f1 - f0, part[k]);
-        end[k] = (size_t)(in.p - src);
-      });
-    }
-    for (auto& t : th) t.join();
-    bool agree = true;
-    for (size_t k = 0; k + 1 < T && agree; k++) {
-      if (st[k]) break;
-      agree = end[k] == starts[starts.size() * (k + 1) / T];
-    }
-    if (agree) {
-      size_t total = 0;
-      for (auto& v : part) total += v.size();
-      P->frames.reserve(total);
-      for (size_t k = 0; k < T; k++) {
-        for (auto& hf : part[k]) P->frames.push_back(std::move(hf));
-        if (st[k]) { P->index_status = st[k]; break; }
+  static const char* wt = getenv("ZD_WALK_THREADS");   // experiments
+  const unsigned hw = wt ? (unsigned)std::max(1, atoi(wt)) : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t T = n >= PAR_INDEX_MIN_BYTES ? std::min<size_t>(hw, n >> 20) : 1;
+  std::vector<HostPart> part(T);
+  std::vector<int> st(T, 0);
+  std::vector<size_t> end(T, 0), cut(T + 1);
+  for (size_t k = 0; k <= T; k++) cut[k] = (size_t)((unsigned __int128)n * k / T);
+  std::vector<double> tms(T, 0.0);
+  const auto tw0 = std::chrono::steady_clock::now();
+  run_parts(T, [&](size_t k) {
+    const auto tk0 = std::chrono::steady_clock::now();
+    struct Stamp {
+      double& out; std::chrono::steady_clock::time_point t0;
+      ~Stamp() { out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } stamp{tms[k], tk0};
+    size_t p = cut[k];
+    for (;;) {
+      if (k) {                                   // the first candidate frame start in the range
+        while (p < cut[k + 1] && (p + 4 > n || !magic_at(src + p))) p++;
+        if (p >= cut[k + 1]) { end[k] = p; return; }
       }
-      P->index_stop = P->frames.size();
-      return 0;
+      part[k].blocks.reserve((cut[k + 1] - cut[k]) / (16u << 10) + 16);
+      Bytes in{src + p, n - p};
+      st[k] = index_frames(src, in, cut[k + 1], part[k]);
+      end[k] = (size_t)(in.p - src);
+      // a candidate that fails at once was a magic inside data: look further
+      if (k && st[k] && part[k].frames.size() == 1) {
+        part[k].frames.clear();
+        part[k].blocks.clear();
+        st[k] = 0;
+        p++;
+        continue;
+      }
+      return;
     }
+  });
+  std::vector<HostPart> keep;
+  int status = 0;
+  size_t cur = 0;                                // where the kept frames end
+  for (size_t k = 0; k < T && !status; k++) {
+    if (k && cur >= cut[k + 1]) continue;        // the range lies inside a kept frame
+    HostPart& hp = part[k];
+    size_t i = 0;
+    while (i < hp.frames.size() && hp.frames[i].d.src_offset < cur) i++;
+    if (k && (i == hp.frames.size() || hp.frames[i].d.src_offset != cur)) {
+      // the chains do not meet: the rest of the input serially
+      HostPart tail;
+      Bytes in{src + cur, n - cur};
+      status = index_frames(src, in, SIZE_MAX, tail);
+      keep.push_back(std::move(tail));
+      cur = n;
+      break;
+    }
+    if (i) hp.frames.erase(hp.frames.begin(), hp.frames.begin() + (long)i);   // their blocks stay unreferenced
+    status = st[k];
+    cur = end[k];
+    keep.push_back(std::move(hp));
   }
-  Bytes in{src, n};
-  P->index_status = index_frames(src, in, SIZE_MAX, P->frames);
-  P->index_stop = P->frames.size();
+  const auto tw1 = std::chrono::steady_clock::now();
+  P->set_parts(std::move(keep));
+  if (getenv("ZD_PLAN_TIMES")) {
+    fprintf(stderr, "zd walk: %zu threads, threads", T);
+    for (double t : tms) fprintf(stderr, " %.1f", t);
+    fprintf(stderr, " ms; walk %.2f ms, stitch %.2f ms\n", std::chrono::duration<double, std::milli>(tw1 - tw0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count());
+  }
+  P->index_status = status;
+  P->index_stop = P->nframes;
   return 0;
 }
 
@@ -747,9 +1161,43 @@ int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
 // ===========================================================================
 // C ABI
 // ===========================================================================
+// Diagnostics (ZD_PLAN_DUMP=path): the plan's descriptor arrays, for
+// comparing planner revisions byte for byte.
+static void dump_plan_desc(const zd_plan* P) {
+  const char* path = getenv("ZD_PLAN_DUMP");
+  if (!path) return;
+  FILE* f = fopen(path, "wb");
+  if (!f) return;
+  auto w = [&](const void* p, size_t bytes) { uint64_t b = bytes; fwrite(&b, 8, 1, f); if (bytes) fwrite(p, 1, bytes, f); };
+  const Workspace& W = P->W;
+  auto at = [&](uint64_t off, const void* vec) -> const void* {
+    return P->staged ? (const void*)(host_stage().p + off) : vec;
+  };
+  w(at(W.comp, P->comps.data()), P->n_comps * sizeof(CompBlock));
+  w(at(W.blocks, P->blocks.data()), P->n_blocks * sizeof(BlockRec));
+  w(at(W.frames, P->fdesc.data()), P->n_frames * sizeof(FrameDesc));
+  w(at(W.frame_state0, P->fstate0.data()), P->n_frames * sizeof(FrameState));
+  w(at(W.list_tables, P->list_tables.data()), P->n_tables * 4);
+  w(at(W.list_huf, P->list_huf.data()), P->n_huf * 4);
+  w(at(W.list_seq, P->list_seq.data()), P->n_seq * 4);
+  w(at(W.list_k4f, P->list_k4f.data()), P->n_k4f * 4);
+  w(at(W.copies, P->copies.data()), P->n_copies * sizeof(CopyDesc));
+  w(at(W.jframes, P->jframes.data()), P->n_jframes * sizeof(JFrame));
+  w(at(W.jblkd, P->jblkd.data()), P->n_jblk * sizeof(JBlkDesc));
+  w(at(W.jsegd, P->jsegd.data()), P->n_jseg * sizeof(JSegDesc));
+  w(P->frame_out.data(), P->frame_out.size() * 8);
+  zd_plan_info I = P->info; I.workspace_bytes = 0; I.host_ns = I.device_ns = 0;
+  w(&I, sizeof I);
+  uint64_t x[4] = {P->j_bytes, P->j_pieces, P->j_rounds, (uint64_t)(int64_t)P->index_status};
+  w(x, sizeof x);
+  fclose(f);
+}
+
 extern "C" {
 
 int zd_abi_version(void) { return ZD_ABI_VERSION; }
+
+void zd_trim_cache(void) { ws_trim(-1); }
 
 const char* zd_status_name(int s) {
   switch (s) {
@@ -790,29 +1238,33 @@ const char* zd_status_name(int s) {
 int zd_frames_index(const uint8_t* src, size_t n, zd_frame_desc* frames, size_t cap_frames, size_t* nframes,
                     zd_block_desc* blocks, size_t cap_blocks, size_t* nblocks, size_t* consumed) {
   if (!src && n) return ZD_E_INVALID_ARG;
-  Bytes in{src, n};
+  zd_plan W;                                     // the host walk only (no device state)
+  plan_index(&W, src, n);
   size_t nf = 0, nb = 0;
   int status = 0;
   size_t stop = n;
-  while (in.n) {
-    if (frames && cap_frames && nf >= cap_frames) { stop = (size_t)(in.p - src); break; }
-    HostFrame hf;
-    size_t at = (size_t)(in.p - src);
-    int r = index_frame(src, in, &hf);
-    if (r) { status = r; stop = at; break; }
-    hf.d.first_block = (uint32_t)nb;
-    hf.d.num_blocks = (uint32_t)hf.blocks.size();
-    if (frames && nf < cap_frames) frames[nf] = hf.d;
-    for (auto& b : hf.blocks) {
-      if (blocks && nb < cap_blocks) {
-        zd_block_desc& d = blocks[nb];
-        d.src_offset = b.src; d.block_size = b.size; d.type = b.type == 4 ? 0 : b.type;
-        d.last = b.last; d.rle_byte = b.rle; d._pad = 0;
+  for (const HostPart& hp : W.parts) {
+    for (const HostFrame& hf : hp.frames) {
+      if (frames && cap_frames && nf >= cap_frames) { stop = (size_t)hf.d.src_offset; goto done; }
+      if (hf.status) { status = hf.status; stop = (size_t)hf.d.src_offset; goto done; }
+      if (frames && nf < cap_frames) {
+        frames[nf] = hf.d;
+        frames[nf].first_block = (uint32_t)nb;
+        frames[nf].num_blocks = hf.nb;
       }
-      nb++;
+      for (uint32_t k = 0; k < hf.nb; k++) {
+        const HostBlock& b = hp.blocks[hf.b0 + k];
+        if (blocks && nb < cap_blocks) {
+          zd_block_desc& d = blocks[nb];
+          d.src_offset = b.src; d.block_size = b.size; d.type = b.type == 4 ? 0 : b.type;
+          d.last = b.last; d.rle_byte = b.rle; d._pad = 0;
+        }
+        nb++;
+      }
+      nf++;
     }
-    nf++;
   }
+done:
   if (nframes) *nframes = nf;
   if (nblocks) *nblocks = nb;
   if (consumed) *consumed = stop;
@@ -829,22 +1281,25 @@ int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) 
   const auto ti = std::chrono::steady_clock::now();
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {1, 4, 8};
-  build_plan(P, -1, none, 0, rep0, 0);
+  if (int r = build_plan(P, -1, none, 0, rep0, 0, true)) { zd_plan_destroy(P); return r; }
   P->info.src_bytes = n;
   const auto t1 = std::chrono::steady_clock::now();
+  dump_plan_desc(P);
   if (getenv("ZD_PLAN_TIMES"))
     fprintf(stderr, "zd plan: index %.2f ms, descriptors %.2f ms\n",
             std::chrono::duration<double, std::milli>(ti - t0).count(),
             std::chrono::duration<double, std::milli>(t1 - ti).count());
   int r = upload_plan(P);
+  const auto tu = std::chrono::steady_clock::now();
   // the second stream and its events (K2 beside K3, opt-in overlap) exist
   // from here on, so zd_decode_async creates nothing
-  if (!r && (hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking) != hipSuccess ||
-             hipEventCreateWithFlags(&P->fork, hipEventDisableTiming) != hipSuccess ||
-             hipEventCreateWithFlags(&P->join, hipEventDisableTiming) != hipSuccess))
-    r = ZD_E_HIP;
+  if (!r && !aux_take(P)) r = ZD_E_HIP;
   if (r) { zd_plan_destroy(P); return r; }
   const auto t2 = std::chrono::steady_clock::now();
+  if (getenv("ZD_PLAN_TIMES"))
+    fprintf(stderr, "zd plan: workspace + upload %.2f ms, streams %.2f ms\n",
+            std::chrono::duration<double, std::milli>(tu - t1).count(),
+            std::chrono::duration<double, std::milli>(t2 - tu).count());
   P->info.host_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
   P->info.device_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
   *out = P;
@@ -859,12 +1314,16 @@ int zd_plan_info_get(const zd_plan* P, zd_plan_info* info) {
 
 void zd_plan_destroy(zd_plan* P) {
   if (!P) return;
-  if (P->d_ws) (void)hipFree(P->d_ws);
+  // the workspace and the second stream go back to process caches: work the
+  // plan launched must be done with them first (hipFree used to imply that)
+  if (P->launched) {
+    (void)hipStreamSynchronize(P->last_stream);
+    if (P->aux) (void)hipStreamSynchronize(P->aux);
+  }
+  ws_release(P->d_ws, P->ws_bytes);
   if (P->d_staging) (void)hipFree(P->d_staging);
   if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
-  if (P->fork) (void)hipEventDestroy(P->fork);
-  if (P->join) (void)hipEventDestroy(P->join);
-  if (P->aux) (void)hipStreamDestroy(P->aux);
+  aux_give(P);
   delete P;
 }
 
@@ -902,9 +1361,9 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // offsets, flags) from device-resident copies: no host memory is read, so
   // a graph captured around this call replays the reset
   HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->d_ws + P->W.frame_state0,
-                        P->fstate0.size() * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
-  if (!P->jframes.empty()) {
+                        P->n_frames * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<uint64_t>(P->n_comps, 1) * sizeof(CompState), s));
+  if (P->n_jframes) {
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jdone, 0, std::max<uint64_t>(P->j_pieces, 1), s));
   }
@@ -914,15 +1373,15 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.out = P->info.out_exact ? d_dst : P->d_staging;
   a.ws = P->d_ws;
   a.W = P->W;
-  a.n_tables = (uint32_t)P->list_tables.size();
-  a.n_huf = (uint32_t)P->list_huf.size();
-  a.n_seq = (uint32_t)P->list_seq.size();
-  a.n_frames = (uint32_t)P->fdesc.size();
-  a.n_k4f = (uint32_t)P->list_k4f.size();
-  a.n_copies = (uint32_t)P->copies.size();
-  a.n_jframes = (uint32_t)P->jframes.size();
-  a.n_jblk = (uint32_t)P->jblkd.size();
-  a.n_jseg = (uint32_t)P->jsegd.size();
+  a.n_tables = (uint32_t)P->n_tables;
+  a.n_huf = (uint32_t)P->n_huf;
+  a.n_seq = (uint32_t)P->n_seq;
+  a.n_frames = (uint32_t)P->n_frames;
+  a.n_k4f = (uint32_t)P->n_k4f;
+  a.n_copies = (uint32_t)P->n_copies;
+  a.n_jframes = (uint32_t)P->n_jframes;
+  a.n_jblk = (uint32_t)P->n_jblk;
+  a.n_jseg = (uint32_t)P->n_jseg;
   a.j_rounds = P->j_rounds;
   a.j_pieces = P->j_pieces;
   // hops per pending word and K4J round (c3s, scripts/exp_jhops.sh: 1 hop
@@ -940,13 +1399,14 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // ZD_FORK=1 / 0 forces it on / off
   static const char* fork_env = getenv("ZD_FORK");
   const bool fork = fork_env ? atoi(fork_env) == 1
-                             : P->list_seq.size() >= FORK_MIN_SEQ_BLOCKS && P->list_seq.size() <= FORK_MAX_SEQ_BLOCKS;
+                             : P->n_seq >= FORK_MIN_SEQ_BLOCKS && P->n_seq <= FORK_MAX_SEQ_BLOCKS;
   static const bool overlap = getenv("ZD_OVERLAP") && atoi(getenv("ZD_OVERLAP")) == 1;
-  if (overlap && !fork && P->fdesc.size() > 1) {
+  if (overlap && !fork && !P->staged && P->n_frames > 1) {
     // K4 of the first half of the frames beside K3 of the second half
-    // (measured slower on C4, 45.1 vs 41.2 ms: both kernels are LDS-bound)
+    // (measured slower on C4, 45.1 vs 41.2 ms: both kernels are LDS-bound;
+    // plans small enough to keep host descriptors only)
     a.overlap = true;
-    a.n_frames_a = (uint32_t)(P->fdesc.size() / 2);
+    a.n_frames_a = (uint32_t)(P->n_frames / 2);
     uint32_t k = 0;
     while (k < P->list_seq.size() && P->comps[P->list_seq[k]].frame < a.n_frames_a) k++;
     a.n_seq_a = k;
@@ -955,6 +1415,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   if (const char* g = getenv("ZD_K4_GRID")) a.k4_grid = (uint32_t)strtoul(g, nullptr, 0);
   HIPCHK(launch_pipeline(a));
   P->launched = true;
+  P->last_stream = s;
   return ZD_OK;
 }
 
@@ -963,7 +1424,7 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
   if (!P || !P->launched) return ZD_E_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipStreamSynchronize(s));
-  size_t nf = P->fdesc.size();
+  size_t nf = P->n_frames;
   std::vector<FrameState> st(nf);
   if (nf) HIPCHK(hipMemcpy(st.data(), P->d_ws + P->W.frame_state, nf * sizeof(FrameState), hipMemcpyDeviceToHost));
   int first = -1;
@@ -979,8 +1440,8 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
     if (frame_len) frame_len[f] = code ? 0 : l;
     if (code && first < 0) { first = (int)f; overall = code; }
     if (first < 0) {
-      if (P->info.out_exact && l != P->fdesc[f].out_cap) need_compact = true;
-      from.push_back(P->fdesc[f].out);
+      if (P->info.out_exact && l != P->frame_cap[f]) need_compact = true;
+      from.push_back(P->frame_out[f]);
       to.push_back(total);
       len.push_back(l);
       total += l;
@@ -1017,7 +1478,7 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
 int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* ok, uint64_t* hash) {
   if (!P || !P->launched) return ZD_E_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const size_t nf = P->fdesc.size(), m = P->res_off.size();   // frames 0..m-1 were decoded
+  const size_t nf = P->n_frames, m = P->res_off.size();   // frames 0..m-1 were decoded
   std::vector<uint64_t> h(m, 0);
   if (m) {
     uint64_t* d = nullptr;
@@ -1031,7 +1492,7 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
     if (e != hipSuccess) return ZD_E_HIP;
   }
   for (size_t f = 0; f < nf; f++) {
-    const zd_frame_desc& d = P->frames[f].d;
+    const zd_frame_desc& d = P->frame(f).d;
     const bool have = f < m && d.kind == ZD_FRAME_ZSTD && d.has_checksum;
     if (ok) ok[f] = have ? ((uint32_t)h[f] == d.checksum ? 1 : 0) : -1;
     if (hash) hash[f] = f < m ? h[f] : 0;
@@ -1236,6 +1697,7 @@ int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consume
   if (last) *last = hb.last;
 
   zd_plan P;
+  HostPart part;
   HostFrame hf;
   memset(&hf.d, 0, sizeof hf.d);
   hf.d.kind = ZD_FRAME_ZSTD;
@@ -1251,13 +1713,20 @@ int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consume
     pre.cb.host_stage = PS_ALL;
     pre.cb.nseq = 1;
     pre.cb.modes[0] = pre.cb.modes[1] = pre.cb.modes[2] = M_FSE;
-    hf.blocks.push_back(pre);
+    part.blocks.push_back(pre);
     P.has_prebuilt = true;
     if (c->has_huf) prev_huf = 0;
     for (int k = 0; k < 3; k++) if (c->has_tab[k]) prev_tab[k] = 0;
   }
-  hf.blocks.push_back(hb);
-  P.frames.push_back(hf);
+  part.blocks.push_back(hb);
+  hf.nb = (uint32_t)part.blocks.size();
+  for (const HostBlock& b : part.blocks) hf.ncomp += b.type == 2;
+  part.frames.push_back(hf);
+  {
+    std::vector<HostPart> one;
+    one.push_back(std::move(part));
+    P.set_parts(std::move(one));
+  }
   // resolve with the prebuilt block as "previous": build_plan walks the blocks in
   // order, so the virtual block seeds Treeless/Repeat through prev_huf/prev_tab.
   uint64_t cap = c->len + (hb.type == 2 ? (uint64_t)MAX_BLOCK_OUT : (uint64_t)hb.size);
@@ -1311,7 +1780,8 @@ int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consume
   }
   P.info.src_bytes = n;
   int r = ctx_run(c, &P, src, n);
-  if (P.d_ws) { (void)hipFree(P.d_ws); P.d_ws = nullptr; }
+  ws_release(P.d_ws, P.ws_bytes);
+  P.d_ws = nullptr;
   if (P.d_staging) { (void)hipFree(P.d_staging); P.d_staging = nullptr; }
   return r;
 }
@@ -1335,8 +1805,16 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   hb.cb.lit_type = LIT_RAW; hb.cb.lit_regen = (uint32_t)nlits; hb.cb.lit_data = 0;
   hb.cb.nseq = (uint32_t)nseq; hb.cb.host_stage = PS_ALL; hb.cb.seq_direct = 1;
   hb.cb.modes[0] = hb.cb.modes[1] = hb.cb.modes[2] = M_RLE;
-  hf.blocks.push_back(hb);
-  P.frames.push_back(hf);
+  HostPart part;
+  part.blocks.push_back(hb);
+  hf.nb = 1;
+  hf.ncomp = 1;
+  part.frames.push_back(hf);
+  {
+    std::vector<HostPart> one;
+    one.push_back(std::move(part));
+    P.set_parts(std::move(one));
+  }
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {c->rep[0], c->rep[1], c->rep[2]};
   build_plan(&P, -1, none, c->len, rep0, c->d_cap);
@@ -1348,7 +1826,7 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   int r = upload_plan(&P);
   auto fin = [&](int rr) {
     if (d_src) (void)hipFree(d_src);
-    if (P.d_ws) (void)hipFree(P.d_ws);
+    ws_release(P.d_ws, P.ws_bytes);
     if (P.d_staging) (void)hipFree(P.d_staging);
     P.d_ws = nullptr; P.d_staging = nullptr;
     return rr;

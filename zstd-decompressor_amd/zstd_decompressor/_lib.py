@@ -58,6 +58,7 @@ _u8p, _sz, _szp, _vp = C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_size_t), 
 SIGNATURES = {
     "zd_status_name": (C.c_char_p, [C.c_int]),
     "zd_abi_version": (C.c_int, []),
+    "zd_trim_cache": (None, []),
     "zd_frames_index": (C.c_int, [_vp, _sz, C.POINTER(FrameDesc), _sz, _szp, C.POINTER(BlockDesc), _sz, _szp, _szp]),
     "zd_plan_create": (C.c_int, [_vp, _sz, C.c_uint32, C.POINTER(_vp)]),
     "zd_plan_info_get": (C.c_int, [_vp, C.POINTER(PlanInfo)]),
