@@ -63,7 +63,10 @@ def make_corpus(workload: str, unique_bytes: int, seed: int, level: int = 9):
         data = libzstd.compress(src, 3)
         return data, src, 1, {"frames": 1, "level": 3}, time.time() - t0
     if workload == "c5":
-        src = gen.text(unique_bytes, seed=seed)
+        # Silesia-style mix (BASELINE.json configs[4]): xml, dickens-like
+        # prose and mozilla-like binary, a third each, 1 MiB frames
+        third = (unique_bytes // 3) >> 20 << 20
+        src = gen.xml(third, seed=seed) + gen.text(third, seed=seed + 1) + gen.binary(unique_bytes - 2 * third, seed=seed + 2)
         data = gen.frames(src, 1 << 20, level)
         return data, src, None, {"frame_bytes": 1 << 20, "level": level}, time.time() - t0
     src = gen.text(unique_bytes, seed=seed)
@@ -201,6 +204,13 @@ def traffic_of(kernel: str, args, world: int):
     except (OSError, ValueError, KeyError):
         return None
     return None if not k else round(k["traffic"] / 1e9, 3)
+
+
+def traffic_commit():
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get("commit")
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -427,7 +437,8 @@ def main():
               "c2": "C2: single 64 MiB frame, 512 alternating raw/RLE 128 KiB blocks",
               "c3": "C3: enwik8-style 100,000,000 B, 763 x 128 KiB frames, zstd -3",
               "c3s": "C3 single frame: enwik8-style 100,000,000 B as ONE zstd -3 frame (763 blocks)",
-              "c5": f"C5: text, 1 MiB multi-block frames, zstd -{args.level}"}[args.workload]
+              "c5": f"C5: Silesia-style mix (xml / prose / binary thirds), 1 MiB multi-block frames, zstd -{args.level}, "
+                    f"{args.unique_mib} MiB unique x{reps}"}[args.workload]
         if world > 1:
             wl += (f", frame-sharded across {world} GPUs" if strong else f", one such corpus per GPU ({world})")
         res = {
@@ -461,7 +472,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic_of(dom, args, world),
-                "traffic_unit": "GB per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, profiles/traffic.json)",
+                "traffic_unit": "GB per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, uncorrected, profiles/traffic.json)",
+                "traffic_commit": traffic_commit(),
                 "alg_bytes_per_launch": int(alg_per_launch),
                 "pipeline_achieved": round(alg_per_launch / (ms_per_step / 1e3) / 1e9, 1),
                 "pipeline_frac": round(alg_per_launch / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
