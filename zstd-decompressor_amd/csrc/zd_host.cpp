@@ -1389,6 +1389,10 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   static const char* hops_env = getenv("ZD_J_HOPS");
   a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 8u;
   a.stream = s;
+  // the pipelined streaming executor K4P, opt-in (ZD_K4P=1, read per launch):
+  // parity-green but slower than K4 on C4
+  const char* k4p_env = getenv("ZD_K4P");
+  a.k4_pipe = k4p_env && atoi(k4p_env) != 0;
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
   // K2 beside K3 on a second stream: measured slower on C4 (61.4 vs 57.9 ms:

@@ -25,6 +25,7 @@ struct LaunchArgs {
   uint32_t n_jframes = 0, n_jblk = 0, n_jseg = 0;   // K4J frames / their blocks / scatter segments
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
+  bool k4_pipe = false;    // streaming frames: the pipelined K4P (K4 for the context API's direct records)
   uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
 };
 
