@@ -1445,7 +1445,25 @@ __device__ __attribute__((always_inline)) inline bool k4_emit_match(WX& X, l_u8*
 
 // Inclusive prefix sum over the 64 lanes (all active) with DPP moves:
 // row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 and 31 across rows.
+#ifndef ZD_K4_DPPASM
+#define ZD_K4_DPPASM 1
+#endif
 __device__ inline uint32_t wave_scan_incl(uint32_t x) {
+#if ZD_K4_DPPASM
+  // one v_add_u32_dpp per step (the builtin form compiles to v_mov_dpp +
+  // v_add); in place, so lanes a row_mask or the row edge leaves out keep x.
+  // s_nop 1: the 2 wait states a DPP read of a just-written VGPR needs.
+  asm volatile(
+      "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\tv_add_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(x));
+  return x;
+#endif
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
@@ -1457,6 +1475,12 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 
 #ifndef ZD_K4_MINW
 #define ZD_K4_MINW 4
+#endif
+#ifndef ZD_K4_CODELUT
+#define ZD_K4_CODELUT 1
+#endif
+#ifndef ZD_K4_INWIN
+#define ZD_K4_INWIN 1
 #endif
 #ifndef ZD_K4_STG
 #define ZD_K4_STG 512                       // C4, 4 GiB: 1024 8.36 ms, 512 8.25, 256 8.24
@@ -1474,8 +1498,25 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
-  __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];      // a batch's literal bytes (K4_STG of them)
+#ifdef ZD_K4_STGFULL
+  __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];
+#else
+  __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
+#endif
   const int lane = threadIdx.x;
+#if ZD_K4_CODELUT
+  // LL | ML code -> baseline | extra-bit count << 24 (ll_code / ml_code,
+  // sequences.rs tables), one LDS read per code instead of ~20 VALU ops
+  __shared__ uint32_t codelut[2][64];
+  {
+    uint32_t b, e;
+    ll_code((uint32_t)lane, &b, &e);
+    codelut[0][lane] = b | (e << 24);
+    ml_code((uint32_t)lane, &b, &e);
+    codelut[1][lane] = b | (e << 24);
+    k4_sync();
+  }
+#endif
   // persistent over frames when the grid is capped
   for (uint32_t f = f_begin + blockIdx.x; f < f_end; f += gridDim.x) {
   const FrameDesc F = frames[f];
@@ -1593,7 +1634,14 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const uint32_t i = s0 + lane;
         const bool valid = i < n;
         K4P(7);
-        *(l_u32x4*)(stg + 16 * lane) = litA;         // this batch's literal bytes from the cursor on
+#ifdef ZD_K4_STGFULL
+        *(l_u32x4*)(stg + 16 * lane) = litA;
+#else
+        // this batch's literal bytes from the cursor on; lanes past the stage
+        // all store into its 16-byte tail (only ever read as overshoot):
+        // unconditional, a branch here cost 4 % of K4
+        *(l_u32x4*)(stg + min(16 * (uint32_t)lane, K4_STG)) = litA;
+#endif
 #ifndef ZD_K4_LATE_FLUSH
         // The previous batch's output goes to HBM here, after the wait for
         // this batch's prefetched loads: those stores then have a batch to
@@ -1627,8 +1675,14 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
             const uint32_t stt = (uint32_t)(recA >> 32);
             const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
             uint32_t llbase, llb, mlbase, mlb;
+#if ZD_K4_CODELUT
+            const uint32_t cl = codelut[0][llc], cm = codelut[1][mlc];
+            llbase = cl & 0xFFFFFF; llb = cl >> 24;
+            mlbase = cm & 0xFFFFFF; mlb = cm >> 24;
+#else
             ll_code(llc, &llbase, &llb);
             ml_code(mlc, &mlbase, &mlb);
+#endif
             uint64_t t = winu_top(winA, 0);
             const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
             ofv = (1u << ofc) + ob;
@@ -1698,6 +1752,14 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           fv0 = ldg16_nt(X.out + slo);
           if (ml > 16) fv1 = ldg16_nt(X.out + slo + 16);
         }
+        // matches whose source lies wholly in the window and before this
+        // batch (written by earlier batches, so no order among the lanes):
+        // copied from LDS in the same pass as the far ones, not in rounds.
+        // Not overlapping (off >= ml): the pass reads four pieces before it
+        // writes them (a lane at the batch start with ll = 0 and off < ml
+        // has shi = q = the batch start)
+        const bool inwin = ZD_K4_INWIN && valid && lane < kk && ml && !far && off32 >= 16 && off32 >= ml &&
+                           off32 <= (uint32_t)q && slo >= X.hs && shi <= X.pos;
         // checks (decoding_context.rs:86-90, D9)
         const uint64_t before = (uint64_t)X.pos + opos;
         const bool dbad = valid && derr != 0;
@@ -1742,17 +1804,30 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         K4P(2);
         // far matches from the bytes loaded above (ml < off: no overlap);
         // the rest in frontier rounds
-        if (far) {
+        if (far || inwin) {
           l_u8* d = X.at(q);
-          sts_n(d, fv0, ml);
-          if (ml > 16) sts_n(d + 16, fv1, ml - 16);
+          u32x4 a0 = fv0;
+          if (inwin) a0 = lds16(X.at(slo));
+          sts_n(d, a0, ml);
+          if (ml > 16) {
+            u32x4 a1 = fv1;
+            if (inwin) a1 = lds16(X.at(slo + 16));
+            sts_n(d + 16, a1, ml - 16);
+          }
           // the rest four pieces at a time: one load latency per 64 bytes
           for (uint32_t x = 32; x < ml; x += 64) {
-            u32x4 v1 = fv0, v2 = fv0, v3 = fv0;
-            const u32x4 v0 = ldg16_nt(X.out + slo + x);
-            if (x + 16 < ml) v1 = ldg16_nt(X.out + slo + x + 16);
-            if (x + 32 < ml) v2 = ldg16_nt(X.out + slo + x + 32);
-            if (x + 48 < ml) v3 = ldg16_nt(X.out + slo + x + 48);
+            u32x4 v0, v1 = fv0, v2 = fv0, v3 = fv0;
+            if (inwin) {
+              v0 = lds16(X.at(slo + (int32_t)x));
+              if (x + 16 < ml) v1 = lds16(X.at(slo + (int32_t)x + 16));
+              if (x + 32 < ml) v2 = lds16(X.at(slo + (int32_t)x + 32));
+              if (x + 48 < ml) v3 = lds16(X.at(slo + (int32_t)x + 48));
+            } else {
+              v0 = ldg16_nt(X.out + slo + x);
+              if (x + 16 < ml) v1 = ldg16_nt(X.out + slo + x + 16);
+              if (x + 32 < ml) v2 = ldg16_nt(X.out + slo + x + 32);
+              if (x + 48 < ml) v3 = ldg16_nt(X.out + slo + x + 48);
+            }
             sts_n(d + x, v0, ml - x);
             if (x + 16 < ml) sts_n(d + x + 16, v1, ml - x - 16);
             if (x + 32 < ml) sts_n(d + x + 32, v2, ml - x - 32);
@@ -1763,7 +1838,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
 #ifdef ZD_EXP_NOROUNDS
         uint64_t done = ~0ull;                    // experiment: no near-match copies
 #else
-        uint64_t done = __ballot(!act || ml == 0 || far);
+        uint64_t done = __ballot(!act || ml == 0 || far || inwin);
 #endif
         k4_sync();
         K4P(3);
