@@ -1008,7 +1008,9 @@ __device__ inline WinN<N> winn_load(const uint8_t* s, int32_t m, int32_t pos) {
 template <int N>
 __device__ inline uint32_t winn_at(const WinN<N>& w, uint32_t y) {
   // (a qword-then-dword select takes fewer instructions but a longer
-  // dependent chain: 14.8 vs 13.8 ms for K3 on C4)
+  // dependent chain: 14.8 vs 13.8 ms for K3 on C4; a threshold tree, the
+  // same 5 compares and 10 selects but 3 deep instead of 5: 5.63 -> 5.99 ms
+  // on 4 GiB)
   uint32_t lo = w.w[0], hi = w.w[1];
 #pragma unroll
   for (int i = 1; i < N; i++) {
@@ -1334,7 +1336,7 @@ struct K4W {
   __device__ inline int32_t space() const { return C - (pos - hs); }
   __device__ inline int32_t alignd(int32_t p) const { return ((p - a0) & ~15) + a0; }
   // 16 bytes of frame output at p (p >= 0): LDS when inside the window, else HBM
-  __device__ inline u32x4 src16(int32_t p) const { return p >= hs ? lds16(at(p)) : ldg16_nt(out + p); }
+  __device__ inline u32x4 src16(int32_t p) const { return p >= hs ? lds16(at(p)) : ldg16_nt(out + (uint32_t)p); }
 };
 typedef K4W<K4_C, K4_W, K4_B> K4;
 
@@ -1699,7 +1701,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const uint32_t tot = ll + ml;
         const uint32_t inc_tot = wave_scan_incl(tot);
         const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
-        const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= (int64_t)X.space() - 16);
+        const uint64_t fitm = __ballot(valid && (int32_t)inc_tot <= X.space() - 16);
         const uint32_t k = (uint32_t)__popcll(fitm);
         const int kk = k ? (int)k : 1;                 // lanes this batch executes
         // decode_offset (decoding_context.rs:50-75): fresh offsets (> 3)
@@ -1749,8 +1751,8 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                          shi <= (X.hs < fl_safe ? X.hs : fl_safe);
         u32x4 fv0, fv1;
         if (far) {
-          fv0 = ldg16_nt(X.out + slo);
-          if (ml > 16) fv1 = ldg16_nt(X.out + slo + 16);
+          fv0 = ldg16_nt(X.out + (uint32_t)slo);
+          if (ml > 16) fv1 = ldg16_nt(X.out + (uint32_t)(slo + 16));
         }
         // matches whose source lies wholly in the window and before this
         // batch (written by earlier batches, so no order among the lanes):
@@ -1760,11 +1762,13 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         // has shi = q = the batch start)
         const bool inwin = ZD_K4_INWIN && valid && lane < kk && ml && !far && off32 >= 16 && off32 >= ml &&
                            off32 <= (uint32_t)q && slo >= X.hs && shi <= X.pos;
-        // checks (decoding_context.rs:86-90, D9)
-        const uint64_t before = (uint64_t)X.pos + opos;
+        // checks (decoding_context.rs:86-90, D9), in 32 bits: positions stay
+        // below 2^31 + 2^25 and off32 saturates (an offset of 2^32 or more
+        // is past any position)
+        const uint32_t before = (uint32_t)X.pos + opos;
         const bool dbad = valid && derr != 0;
-        const bool imp = valid && !dbad && ((uint64_t)lit_cursor + lpos + ll > nl || off > before + ll);
-        const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
+        const bool imp = valid && !dbad && (lit_cursor + lpos + ll > nl || off32 > before + ll);
+        const bool panic = valid && !dbad && !imp && ml != 0 && off32 == 0;
         const uint64_t badm = __ballot(dbad || imp || panic);
         if (badm) {
           const int b = __ffsll((long long)badm) - 1;
@@ -1823,10 +1827,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
               if (x + 32 < ml) v2 = lds16(X.at(slo + (int32_t)x + 32));
               if (x + 48 < ml) v3 = lds16(X.at(slo + (int32_t)x + 48));
             } else {
-              v0 = ldg16_nt(X.out + slo + x);
-              if (x + 16 < ml) v1 = ldg16_nt(X.out + slo + x + 16);
-              if (x + 32 < ml) v2 = ldg16_nt(X.out + slo + x + 32);
-              if (x + 48 < ml) v3 = ldg16_nt(X.out + slo + x + 48);
+              const uint8_t* sp = X.out + (uint32_t)slo;
+              v0 = ldg16_nt(sp + x);
+              if (x + 16 < ml) v1 = ldg16_nt(sp + x + 16);
+              if (x + 32 < ml) v2 = ldg16_nt(sp + x + 32);
+              if (x + 48 < ml) v3 = ldg16_nt(sp + x + 48);
             }
             sts_n(d + x, v0, ml - x);
             if (x + 16 < ml) sts_n(d + x + 16, v1, ml - x - 16);
