@@ -1278,6 +1278,13 @@ __device__ inline void sts_n(l_u8* p, u32x4 v, uint32_t n) {
   if (n & 1) { *p = (uint8_t)v.x; }
 }
 __device__ inline void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The smallest multiple of the period off (1..15) that is >= 16, without a
+// division (the compiler hoisted the division out of the rounds loop, ~25
+// VALU ops per batch): 2 off from 8 on, else 5-bit entries of a constant.
+__device__ inline uint32_t period16(uint32_t off) {
+  constexpr uint64_t T = 16ull | 16ull << 5 | 18ull << 10 | 16ull << 15 | 20ull << 20 | 18ull << 25 | 21ull << 30;
+  return off >= 8 ? 2 * off : (uint32_t)(T >> (5 * ((off - 1) & 7))) & 31;
+}
 __device__ inline int64_t readlane_i64(int64_t x, int l) {
   int lo = __shfl((int)(uint32_t)x, l, 64);
   int hi = __shfl((int)(uint32_t)((uint64_t)x >> 32), l, 64);
@@ -1856,7 +1863,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
             if (off32 >= 16) {
               for (uint32_t x = 0; x < ml; x += 16) sts_n(d + x, X.src16(slo + (int32_t)x), ml - x);
             } else {                             // small period: first 16 bytes bytewise, then 16-byte steps
-              const uint32_t m16 = off32 * ((16 + off32 - 1) / off32);
+              const uint32_t m16 = period16(off32);
               const uint32_t head = ml < 16 ? ml : 16;
               uint32_t r = 0;
               for (uint32_t x = 0; x < head; x++) {
@@ -2257,7 +2264,7 @@ __global__ __launch_bounds__(64, ZD_K4P_MINW) void zd_k_execute_pipe(const uint8
           if (off32 >= 16) {
             for (uint32_t x = 0; x < ml; x += 16) sts_n(dd + x, X.src16(slo + (int32_t)x), ml - x);
           } else {                                   // small period: first 16 bytes bytewise, then 16-byte steps
-            const uint32_t m16 = off32 * ((16 + off32 - 1) / off32);
+            const uint32_t m16 = period16(off32);
             const uint32_t head = ml < 16 ? ml : 16;
             uint32_t r = 0;
             for (uint32_t x = 0; x < head; x++) {
