@@ -309,6 +309,19 @@ def main():
     d_dst = torch.empty(info.out_bytes + 64, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    # the same plan with the frame/block header walk on the GPU
+    # (zd_plan_create_device: the input is resident in HBM), warm
+    dev_plan_ms = None
+    if not args.experiment:
+        torch.cuda.synchronize(dev)
+        for _ in range(2):
+            t0 = time.time()
+            dplan = Plan.from_device(d_src.data_ptr(), len(data), stream=sptr)
+            dev_plan_ms = (time.time() - t0) * 1e3
+            dinfo = dplan.info
+            dplan.close()
+            assert (dinfo.nframes, dinfo.nblocks, dinfo.nsequences, dinfo.out_bytes) == \
+                (info.nframes, info.nblocks, info.nsequences, info.out_bytes)
 
     def step():
         plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), info.out_bytes, sptr)
@@ -481,6 +494,7 @@ def main():
             "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
             "host_plan_ms": round(host_plan_s * 1e3, 1),
             "host_plan_first_ms": round(host_plan_first_s * 1e3, 1),
+            "device_walk_plan_ms": None if dev_plan_ms is None else round(dev_plan_ms, 1),
             "host_plan_split_ms": {"headers_and_descriptors": round(info.host_ns / 1e6, 1),
                                    "workspace_alloc_and_upload": round(info.device_ns / 1e6, 1)},
             "value_incl_host_plan": round(total_out.item() / (ms_per_step / 1e3 + host_plan_s) / 1e6, 1),

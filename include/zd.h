@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 3
+#define ZD_ABI_VERSION 4
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -168,6 +168,17 @@ typedef struct zd_plan_info {
  * Host-side work only (no kernel launches).  A frame that fails to index
  * ends the plan (its status is kept and reported by zd_plan_results). */
 int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out);
+/* The same plan from an input resident in device memory only (d_src,
+ * readable for n + ZD_SRC_PADDING bytes): the frame / block header walk runs
+ * on the GPU (zd_k_walk, one wave per byte range, the host walk's own code in
+ * zd_walk.h), and only its index -- frames and blocks, about 150 bytes per
+ * block -- comes back to the host for the descriptors.  Replaces the host
+ * pre-pass of FrameIterator / Frame::parse / Header::parse / Block::parse
+ * and the section headers (frame.rs:61-230, block.rs:43-72,
+ * literals.rs:88-206, sequences.rs:52-143) for input that never was in host
+ * memory (e.g. a frame range received from another GPU).  The plan equals
+ * zd_plan_create's on the same bytes.  Synchronises `stream`. */
+int zd_plan_create_device(const uint8_t* d_src, size_t n, uint32_t flags, void* stream, zd_plan** out);
 int zd_plan_info_get(const zd_plan* plan, zd_plan_info* info);
 /* Waits for the work the plan launched, then returns its device workspace to
  * the process cache (zd_trim_cache). */

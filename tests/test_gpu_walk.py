@@ -1,0 +1,70 @@
+"""The device header walk (zd_plan_create_device, zd_kernels.hip zd_k_walk):
+the frame / block header walk and the section-header parse on the GPU for an
+input resident in HBM (frame.rs:61-230, block.rs:43-72,
+literals.rs:88-206, sequences.rs:52-143).  Its plan must equal the host
+walk's (zd_plan_create) descriptor for descriptor (ZD_PLAN_DUMP) on every
+input: the reference's resources, libzstd frames of every shape, magic numbers
+planted inside compressed data, frames longer than a walk range, skippable
+frames, corruptions and truncations (tests/test_host_walk.py's inputs); and a
+decode through it must give the host plan's output and status.
+"""
+import os
+
+import pytest
+
+from corpus import gen, libzstd
+
+pytestmark = pytest.mark.gpu
+
+
+def _dump(path, make):
+    os.environ["ZD_PLAN_DUMP"] = path
+    try:
+        plan = make()
+    finally:
+        del os.environ["ZD_PLAN_DUMP"]
+    return plan, open(path, "rb").read()
+
+
+def _decode(plan, d_src, dev):
+    import torch
+    n = plan.info.out_bytes
+    d_dst = torch.zeros(n + 64, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), n, s)
+    st, total, fst, flen, first = plan.results(d_dst.data_ptr(), s)
+    return st, bytes(d_dst[:total].cpu().numpy().tobytes()), fst, flen, first
+
+
+def _inputs(resources):
+    for name, data in resources.items():
+        yield name, data
+    yield "empty", b""
+    yield "three bytes", b"\x28\xb5\x2f"
+    yield "one frame", libzstd.compress(gen.text(200 << 10, seed=91), 3)
+    yield "multi-block frames", gen.frames(gen.text(3 << 20, seed=92), 1 << 20, 9)
+    yield "raw/rle", libzstd.compress(gen.binary(300 << 10, seed=93), 1) + libzstd.compress(bytes(500 << 10), 3)
+    import test_host_walk
+    yield from test_host_walk._inputs()
+
+
+def test_device_walk_plan_equals_host_walk(resources, tmp_path):
+    import torch
+    from zstd_decompressor.batch import Plan
+    dev = torch.device("cuda", 0)
+    for name, data in _inputs(resources):
+        for skip in (False, True):
+            d_src = torch.zeros(len(data) + 64, dtype=torch.uint8, device=dev)
+            if data:
+                d_src[: len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+            torch.cuda.synchronize(dev)
+            hp, hd = _dump(str(tmp_path / "h.bin"), lambda: Plan(data, skip))
+            dp, dd = _dump(str(tmp_path / "d.bin"),
+                           lambda: Plan.from_device(d_src.data_ptr(), len(data), skip,
+                                                    stream=torch.cuda.current_stream(dev).cuda_stream))
+            assert dd == hd, f"{name} (-p {skip}): device-walk plan differs from the host walk's"
+            assert dp.info.index_status == hp.info.index_status, name
+            if not skip and len(data) < (8 << 20):
+                assert _decode(dp, d_src, dev) == _decode(hp, d_src, dev), name
+            hp.close()
+            dp.close()

@@ -24,56 +24,11 @@
 #include "../../include/zd.h"
 #include "zd_common.h"
 #include "zd_launch.h"
+#include "zd_walk.h"
 
 using namespace zd;
 
 namespace {
-
-constexpr uint32_t MAGIC_ZSTD = 0xFD2FB528u;   // frame.rs:41
-constexpr uint32_t MAGIC_SKIP = 0x184D2A50u;   // frame.rs:42
-
-struct Err {
-  int code = 0;
-  uint32_t stage = PS_STRUCT;
-};
-
-// ForwardByteParser (parsing.rs:9-112)
-struct Bytes {
-  const uint8_t* p;
-  size_t n;
-  int u8(uint8_t* v) {
-    if (!n) return ZD_E_NOT_ENOUGH_BYTES;
-    *v = *p++; n--; return 0;
-  }
-  int slice(size_t len, const uint8_t** s) {
-    if (len == 0) return ZD_E_EMPTY_SLICE;
-    if (n < len) return ZD_E_NOT_ENOUGH_BYTES;
-    *s = p; p += len; n -= len; return 0;
-  }
-  int le(size_t k, uint64_t* v) {
-    if (n < k) return ZD_E_NOT_ENOUGH_BYTES;
-    uint64_t r = 0;
-    for (size_t i = 0; i < k; i++) r |= (uint64_t)p[i] << (8 * i);
-    p += k; n -= k; *v = r; return 0;
-  }
-};
-
-struct HostBlock {
-  uint64_t src;          // absolute offset of the block content
-  uint32_t size;
-  uint8_t type, last, rle;
-  // compressed only
-  CompBlock cb;
-};
-
-// A frame; its blocks are blocks[b0, b0 + nb) of the part that holds it.
-struct HostFrame {
-  zd_frame_desc d;
-  uint32_t b0 = 0, nb = 0;
-  uint32_t ncomp = 0;         // compressed blocks
-  uint64_t key = KEY_NONE;    // host-detected parse error (frame stops here)
-  int status = 0;
-};
 
 // Frames indexed by one thread of the host walk: a contiguous run of the
 // input's frames and their blocks, stored flat.
@@ -82,247 +37,12 @@ struct HostPart {
   std::vector<HostBlock> blocks;
 };
 
-// Literals section header + the host-visible parts of the section
-// (literals.rs:88-206) and of the sequences header (sequences.rs:52-87 and
-// the mode byte of 91-143).  `c` spans the block content.
-int parse_compressed(const uint8_t* base, uint64_t off, uint32_t size, CompBlock* cb, Err* e) {
-  Bytes np{base + off, size};
-  const uint8_t* start = np.p;
-  auto rel = [&]() { return (uint32_t)(np.p - start); };
-  e->stage = PS_STRUCT;
-  uint8_t h;
-  if (int r = np.u8(&h)) return e->code = r;
-  int lt = h & 3, sf = (h >> 2) & 3;
-  uint32_t regen = 0, csize = 0;
-  int nstreams = 1;
-  if (lt == LIT_RAW || lt == LIT_RLE) {
-    uint8_t b1, b2;
-    if (sf == 0 || sf == 2) regen = h >> 3;
-    else if (sf == 1) { if (int r = np.u8(&b1)) return e->code = r; regen = (h >> 4) + ((uint32_t)b1 << 4); }
-    else {
-      if (int r = np.u8(&b1)) return e->code = r;
-      if (int r = np.u8(&b2)) return e->code = r;
-      regen = (h >> 4) + ((uint32_t)b1 << 4) + ((uint32_t)b2 << 12);
-    }
-  } else {
-    const uint8_t* s;
-    uint32_t nb = sf <= 1 ? 2 : (uint32_t)sf + 1;
-    if (int r = np.slice(nb, &s)) return e->code = r;
-    uint32_t x = 0;
-    for (uint32_t i = 0; i < nb; i++) x |= (uint32_t)s[i] << (8 * i);
-    if (sf <= 1) { regen = (h >> 4) + ((x & 0x3F) << 4); csize = x >> 6; nstreams = sf == 0 ? 1 : 4; }
-    else if (sf == 2) { regen = (h >> 4) + ((x & 0x3FF) << 4); csize = (x >> 10) & 0x3FFF; nstreams = 4; }
-    else { regen = (h >> 4) + ((x & 0x3FFF) << 4); csize = (x >> 14) & 0x3FFFF; nstreams = 4; }
-  }
-  cb->lit_type = (uint8_t)lt;
-  cb->lit_regen = regen;
-  cb->nstreams = 0;
-  if (lt == LIT_RAW) {
-    const uint8_t* s;
-    cb->lit_data = rel();
-    if (int r = np.slice(regen, &s)) return e->code = r;
-  } else if (lt == LIT_RLE) {
-    if (int r = np.u8(&cb->lit_rle)) return e->code = r;
-  } else {
-    const uint8_t* cs;
-    if (int r = np.slice(csize, &cs)) return e->code = r;
-    Bytes ni{cs, csize};
-    const uint8_t* ni_start = cs;
-    if (lt == LIT_COMPRESSED) {      // HuffmanDecoder::parse header + description slice (huffman.rs:80-130)
-      e->stage = PS_HUF_DESC;
-      cb->lit_data = (uint32_t)(cs - start);
-      uint8_t hh;
-      if (int r = ni.u8(&hh)) return e->code = r;
-      size_t dl = hh < 128 ? hh : ((size_t)(hh - 127) / 2 + (hh - 127) % 2);
-      const uint8_t* d;
-      if (int r = ni.slice(dl, &d)) return e->code = r;
-      cb->huf_desc_size = (uint32_t)(1 + dl);
-    }
-    e->stage = PS_JUMP;
-    size_t total = ni.n;
-    uint32_t ss[4] = {0, 0, 0, 0};
-    if (nstreams == 4) {
-      uint64_t s1, s2, s3;
-      if (int r = ni.le(2, &s1)) return e->code = r;
-      if (int r = ni.le(2, &s2)) return e->code = r;
-      if (int r = ni.le(2, &s3)) return e->code = r;
-      if (s1 + s2 + s3 > total - 6) return e->code = ZD_E_CORRUPTED_STREAMS_SIZE;
-      size_t s4 = total - 6 - s1 - s2 - s3;
-      ss[0] = (uint32_t)s1; ss[1] = (uint32_t)s2; ss[2] = (uint32_t)s3; ss[3] = (uint16_t)s4;
-    } else {
-      ss[0] = (uint16_t)ni.n;
-    }
-    cb->streams = (uint32_t)(ni.p - start);
-    const uint8_t* d;
-    if (int r = ni.slice(ni.n, &d)) return e->code = r;
-    (void)ni_start;
-    // literals.rs:70-73: the stream loop stops at the first empty stream
-    for (int k = 0; k < 4; k++) {
-      if (ss[k] == 0) break;
-      cb->stream_size[k] = ss[k];
-      cb->nstreams = (uint8_t)(k + 1);
-    }
-  }
-  // Sequences::parse (sequences.rs:52-75)
-  e->stage = PS_SEQ_HDR;
-  uint8_t b0;
-  if (int r = np.u8(&b0)) return e->code = r;
-  uint32_t nseq;
-  if (b0 == 0) nseq = 0;
-  else if (b0 < 128) nseq = b0;
-  else if (b0 < 255) { uint8_t b1; if (int r = np.u8(&b1)) return e->code = r; nseq = ((uint32_t)(b0 - 128) << 8) + b1; }
-  else {
-    uint8_t b1, b2;
-    if (int r = np.u8(&b1)) return e->code = r;
-    if (int r = np.u8(&b2)) return e->code = r;
-    nseq = (uint32_t)b1 + ((uint32_t)b2 << 8) + 0x7F;     // D1 (sequences.rs:84)
-  }
-  cb->nseq = nseq;
-  cb->modes[0] = cb->modes[1] = cb->modes[2] = M_REPEAT;
-  if (nseq) {
-    const uint8_t* mb;
-    if (int r = np.slice(1, &mb)) return e->code = r;
-    if (mb[0] & 3) return e->code = ZD_E_SEQ_RESERVED_SET;
-    cb->modes[0] = (mb[0] >> 6) & 3;
-    cb->modes[1] = (mb[0] >> 4) & 3;
-    cb->modes[2] = (mb[0] >> 2) & 3;
-  }
-  cb->seq_tables = rel();
-  return 0;
-}
-
-// Header::parse (frame.rs:111-177)
-int parse_header(Bytes& in, zd_frame_desc* f) {
-  const uint8_t* b;
-  if (int r = in.slice(1, &b)) return r;
-  unsigned fhd = b[0];
-  unsigned dict_flag = fhd & 3, csum = (fhd >> 2) & 1, reserved = (fhd >> 3) & 1;
-  unsigned single = (fhd >> 5) & 1, fcs_flag = fhd >> 6;
-  if (reserved) return ZD_E_FRAME_RESERVED_SET;
-  int fcs_size = (fcs_flag == 0) ? (single ? 1 : -1) : (1 << fcs_flag);
-  uint64_t window = 0;
-  if (!single) {
-    uint8_t wd;
-    if (int r = in.u8(&wd)) return r;
-    uint64_t base = 1ull << ((wd >> 3) + 10);
-    window = base + (base / 8) * (wd & 7);
-  }
-  f->dict_id = UINT64_MAX;
-  if (dict_flag) {
-    const uint8_t* a;
-    size_t dl = (size_t)1 << (dict_flag - 1);
-    if (int r = in.slice(dl, &a)) return r;
-    uint64_t v = 0;
-    for (size_t i = 0; i < dl; i++) v |= (uint64_t)a[i] << (8 * i);
-    f->dict_id = v;
-  }
-  f->content_size = UINT64_MAX;
-  if (fcs_size > 0) {
-    const uint8_t* a;
-    if (int r = in.slice((size_t)fcs_size, &a)) return r;
-    uint64_t v = 0;
-    for (int i = 0; i < fcs_size; i++) v |= (uint64_t)a[i] << (8 * i);
-    if (fcs_size == 2) v += 256;
-    f->content_size = v;
-  }
-  f->window_size = single ? f->content_size : window;
-  f->has_checksum = csum;
-  return 0;
-}
-
-// Walks one frame at in, appending its blocks to `blocks`.  On error,
-// hf->key/status hold the failure; blocks parsed before (and the failing one,
-// with its host_stage) are kept.
-int index_frame(const uint8_t* base, Bytes& in, HostFrame* hf, std::vector<HostBlock>& blocks) {
-  zd_frame_desc& f = hf->d;
-  memset(&f, 0, sizeof f);
-  f.src_offset = (uint64_t)(in.p - base);
-  f.content_size = UINT64_MAX;
-  f.dict_id = UINT64_MAX;
-  hf->b0 = (uint32_t)blocks.size();
-  hf->nb = 0;
-  hf->ncomp = 0;
-  auto push = [&](const HostBlock& hb) {
-    blocks.push_back(hb);
-    hf->nb++;
-    hf->ncomp += hb.type == 2;
-  };
-  auto fail = [&](int code, uint32_t blk, uint32_t stage) {
-    hf->status = code;
-    hf->key = make_key(PH_PARSE, blk, stage, 0, code);
-    f.src_size = (uint64_t)(in.p - base) - f.src_offset;
-    return code;
-  };
-  uint64_t magic;
-  if (int r = in.le(4, &magic)) return fail(r, 0, PS_STRUCT);
-  f.magic = (uint32_t)magic;
-  if (f.magic == MAGIC_ZSTD) {
-    f.kind = ZD_FRAME_ZSTD;
-    if (int r = parse_header(in, &f)) return fail(r, 0, PS_STRUCT);
-    if (f.window_size > MAX_WIN_SIZE) return fail(ZD_E_WINDOW_SIZE_TOO_BIG, 0, PS_STRUCT);
-    for (uint32_t bi = 0;; bi++) {
-      const uint8_t* h;
-      if (int r = in.slice(3, &h)) return fail(r, bi, PS_STRUCT);
-      uint32_t x = h[0] | (h[1] << 8) | ((uint32_t)h[2] << 16);
-      HostBlock hb;
-      memset(&hb, 0, sizeof hb);
-      hb.last = x & 1;
-      hb.type = (x >> 1) & 3;
-      hb.size = x >> 3;
-      hb.src = (uint64_t)(in.p - base);
-      // the next block (or frame) header: a cache miss that now overlaps
-      // this block's own header parse
-      if (hb.type != 1 && hb.size < in.n) __builtin_prefetch(in.p + hb.size);
-      if (hb.type == 0) {
-        const uint8_t* s;
-        if (int r = in.slice(hb.size, &s)) return fail(r, bi, PS_STRUCT);
-      } else if (hb.type == 1) {
-        if (int r = in.u8(&hb.rle)) return fail(r, bi, PS_STRUCT);
-      } else if (hb.type == 2) {
-        const uint8_t* s;
-        if (int r = in.slice(hb.size, &s)) return fail(r, bi, PS_STRUCT);
-        CompBlock& cb = hb.cb;
-        cb.src = hb.src;
-        cb.size = hb.size;
-        cb.block_in_frame = bi;
-        cb.host_stage = PS_ALL;
-        Err e;
-        int r = parse_compressed(base, hb.src, hb.size, &cb, &e);
-        if (r) {
-          cb.host_stage = (uint8_t)e.stage;
-          push(hb);
-          return fail(r, bi, e.stage);
-        }
-      } else {
-        return fail(ZD_E_RESERVED_BLOCK_TYPE, bi, PS_STRUCT);
-      }
-      push(hb);
-      if (hb.last) break;
-    }
-    if (f.has_checksum) {
-      uint64_t cs;
-      if (in.le(4, &cs)) return fail(ZD_E_MISSING_CHECKSUM, hf->nb, PS_STRUCT);
-      f.checksum = (uint32_t)cs;
-    }
-  } else if ((f.magic ^ MAGIC_SKIP) <= 0x0F) {
-    f.kind = ZD_FRAME_SKIPPABLE;
-    uint64_t len;
-    if (int r = in.le(4, &len)) return fail(r, 0, PS_STRUCT);
-    const uint8_t* s;
-    HostBlock hb;
-    memset(&hb, 0, sizeof hb);
-    hb.src = (uint64_t)(in.p - base);
-    if (int r = in.slice((size_t)len, &s)) return fail(r, 0, PS_STRUCT);
-    hb.type = 4;
-    hb.size = (uint32_t)len;
-    hb.last = 1;
-    push(hb);
-  } else {
-    return fail(ZD_E_UNRECOGNIZED_MAGIC, 0, PS_STRUCT);
-  }
-  f.src_size = (uint64_t)(in.p - base) - f.src_offset;
-  return 0;
-}
+// The host walk's block sink: a part's block vector
+struct VecSink {
+  std::vector<HostBlock>& v;
+  size_t size() const { return v.size(); }
+  void push(const HostBlock& b) { v.push_back(b); }
+};
 
 #define HIPCHK(x) do { hipError_t _e = (x); if (_e != hipSuccess) { \
   fprintf(stderr, "zd: %s failed: %s\n", #x, hipGetErrorString(_e)); return ZD_E_HIP; } } while (0)
@@ -1061,7 +781,8 @@ void aux_give(zd_plan* P) {
 int index_frames(const uint8_t* src, Bytes& in, size_t stop, HostPart& part) {
   while (in.n && (size_t)(in.p - src) < stop) {
     HostFrame hf;
-    int r = index_frame(src, in, &hf, part.blocks);
+    VecSink sink{part.blocks};
+    int r = index_frame(src, in, &hf, sink);
     part.frames.push_back(hf);
     if (r) return r;
   }
@@ -1071,7 +792,7 @@ int index_frames(const uint8_t* src, Bytes& in, size_t stop, HostPart& part) {
 inline bool magic_at(const uint8_t* p) {
   uint32_t m;
   memcpy(&m, p, 4);
-  return m == MAGIC_ZSTD || (m ^ MAGIC_SKIP) <= 0x0F;
+  return magic_word(m);
 }
 
 // The host walk (FrameIterator over the whole input).  Large inputs are cut
@@ -1151,6 +872,167 @@ int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
     fprintf(stderr, " ms; walk %.2f ms, stitch %.2f ms\n", std::chrono::duration<double, std::milli>(tw1 - tw0).count(),
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count());
   }
+  P->index_status = status;
+  P->index_stop = P->nframes;
+  return 0;
+}
+
+// The device walk (zd_kernels.hip zd_k_walk): plan_index for an input that
+// is resident in HBM.  Byte ranges of >= 256 KiB (at most 16384 of them),
+// one wave each; the count pass gives every range's chain (WalkRange), the
+// fill pass writes their frames and blocks into one array each, which come
+// back to the host through pinned staging.  The stitch is plan_index's, over
+// the ranges; where two chains do not meet, the rest of the input is walked
+// serially on the device (one range from there to the end).  The kept frames
+// are then cut into parts for the parallel descriptor build.
+struct DevWalkBufs {                      // device and pinned buffers, kept between plans
+  std::mutex m;
+  int dev = -1;
+  WalkRange* d_wr = nullptr;
+  size_t cap_wr = 0;
+  uint8_t* d_out = nullptr;              // frames | blocks
+  size_t cap_out = 0;
+  uint8_t* h_out = nullptr;              // pinned
+  size_t cap_h = 0;
+  WalkRange* h_wr = nullptr;             // pinned
+  size_t cap_hwr = 0;
+};
+DevWalkBufs& dev_walk_bufs() {
+  static DevWalkBufs* b = new DevWalkBufs();
+  return *b;
+}
+
+template <typename T>
+bool grow_dev(T*& p, size_t& cap, size_t need) {
+  if (need <= cap) return true;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  const size_t n = std::max(need, cap * 2);
+  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return false;
+  cap = n;
+  return true;
+}
+template <typename T>
+bool grow_pinned(T*& p, size_t& cap, size_t need) {
+  if (need <= cap) return true;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  const size_t n = std::max(need, cap * 2);
+  if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) return false;
+  cap = n;
+  return true;
+}
+
+// Walks `nranges` ranges from `first`; on return wr (pinned) holds the
+// summaries with f_off / b_off, frames / blocks (pinned) the fill pass.
+int dev_walk(DevWalkBufs& B, const uint8_t* d_src, uint64_t n, uint64_t first, uint64_t chunk, uint32_t nranges,
+             hipStream_t s, uint64_t* F_out, uint64_t* B_out, const HostFrame** frames, const HostBlock** blocks) {
+  if (!grow_dev(B.d_wr, B.cap_wr, nranges) || !grow_pinned(B.h_wr, B.cap_hwr, nranges)) return ZD_E_HIP;
+  if (launch_walk(d_src, n, first, chunk, nranges, B.d_wr, nullptr, nullptr, false, s) != hipSuccess ||
+      hipMemcpyAsync(B.h_wr, B.d_wr, nranges * sizeof(WalkRange), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return ZD_E_HIP;
+  uint64_t F = 0, NB = 0;
+  for (uint32_t k = 0; k < nranges; k++) {
+    B.h_wr[k].f_off = F; B.h_wr[k].b_off = NB;
+    F += B.h_wr[k].nframes; NB += B.h_wr[k].nblocks;
+  }
+  const size_t fb = align_up(F * sizeof(HostFrame), 256), bytes = fb + NB * sizeof(HostBlock);
+  *F_out = F;
+  *B_out = NB;
+  if (!F) return 0;
+  if (!grow_dev(B.d_out, B.cap_out, bytes) || !grow_pinned(B.h_out, B.cap_h, bytes)) return ZD_E_HIP;
+  HostFrame* d_frames = (HostFrame*)B.d_out;
+  HostBlock* d_blocks = (HostBlock*)(B.d_out + fb);
+  if (hipMemcpyAsync(B.d_wr, B.h_wr, nranges * sizeof(WalkRange), hipMemcpyHostToDevice, s) != hipSuccess ||
+      launch_walk(d_src, n, first, chunk, nranges, B.d_wr, d_frames, d_blocks, true, s) != hipSuccess ||
+      hipMemcpyAsync(B.h_out, B.d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return ZD_E_HIP;
+  *frames = (const HostFrame*)B.h_out;
+  *blocks = (const HostBlock*)(B.h_out + fb);
+  return 0;
+}
+
+// Frames fr[i] (i in the kept list) with their blocks (global indices into
+// bl) -> parts of about equal frame counts, built in parallel, b0 rebased.
+void parts_from(const std::vector<const HostFrame*>& kept, const HostBlock* bl, std::vector<HostPart>& out) {
+  const size_t nf = kept.size();
+  const size_t T = std::max<size_t>(1, std::min<size_t>(16, nf / 512));
+  const size_t base = out.size();
+  out.resize(base + T);
+  run_parts(T, [&](size_t t) {
+    const size_t a = nf * t / T, e = nf * (t + 1) / T;
+    HostPart& hp = out[base + t];
+    size_t nb = 0;
+    for (size_t i = a; i < e; i++) nb += kept[i]->nb;
+    hp.frames.resize(e - a);
+    hp.blocks.resize(nb);
+    size_t b = 0;
+    for (size_t i = a; i < e; i++) {
+      HostFrame f = *kept[i];
+      memcpy(hp.blocks.data() + b, bl + f.b0, f.nb * sizeof(HostBlock));
+      f.b0 = (uint32_t)b;
+      b += f.nb;
+      hp.frames[i - a] = f;
+    }
+  });
+}
+
+int plan_index_dev(zd_plan* P, const uint8_t* d_src, size_t n, hipStream_t s) {
+  const auto tw0 = std::chrono::steady_clock::now();
+  std::vector<HostPart> keep;
+  int status = 0;
+  double t_walk = 0, t_tail = 0;
+  if (n) {
+    DevWalkBufs& B = dev_walk_bufs();
+    std::lock_guard<std::mutex> lk(B.m);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (B.dev != dev) {                      // buffers of another device: start over
+      B.d_wr = nullptr; B.cap_wr = 0; B.d_out = nullptr; B.cap_out = 0;
+      B.dev = dev;
+    }
+    const uint64_t chunk = std::max<uint64_t>(256u << 10, (n + 16383) / 16384);
+    const uint32_t T = (uint32_t)((n + chunk - 1) / chunk);
+    uint64_t F = 0, NB = 0;
+    const HostFrame* fr = nullptr;
+    const HostBlock* bl = nullptr;
+    if (int r = dev_walk(B, d_src, n, 0, chunk, T, s, &F, &NB, &fr, &bl)) return r;
+    t_walk = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
+    const auto cut = [&](size_t k) { return std::min<uint64_t>((uint64_t)k * chunk, n); };
+    std::vector<const HostFrame*> kept;
+    kept.reserve(F);
+    size_t cur = 0;
+    bool tail = false;
+    for (size_t k = 0; k < T && !status; k++) {
+      const WalkRange& R = B.h_wr[k];
+      if (k && cur >= cut(k + 1)) continue;          // the range lies inside a kept frame
+      const HostFrame* rf = fr + R.f_off;
+      size_t i = 0;
+      while (i < R.nframes && rf[i].d.src_offset < cur) i++;
+      if (k && (i == R.nframes || rf[i].d.src_offset != cur)) { tail = true; break; }
+      for (; i < R.nframes; i++) kept.push_back(rf + i);
+      status = R.status;
+      cur = R.end;
+    }
+    parts_from(kept, bl, keep);
+    if (tail) {                                      // the chains do not meet: the rest serially
+      const auto tt = std::chrono::steady_clock::now();
+      if (int r = dev_walk(B, d_src, n, cur, n - cur, 1, s, &F, &NB, &fr, &bl)) return r;
+      status = B.h_wr[0].status;
+      kept.clear();
+      for (uint64_t i = 0; i < F; i++) kept.push_back(fr + i);
+      parts_from(kept, bl, keep);
+      t_tail = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tt).count();
+    }
+  }
+  P->set_parts(std::move(keep));
+  if (getenv("ZD_PLAN_TIMES"))
+    fprintf(stderr, "zd device walk: %.2f ms (kernels + index download %.2f, serial tail %.2f)\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count(), t_walk, t_tail);
   P->index_status = status;
   P->index_stop = P->nframes;
   return 0;
@@ -1271,13 +1153,19 @@ done:
   return status;
 }
 
-int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) {
-  if (!out || (!src && n)) return ZD_E_INVALID_ARG;
+// zd_plan_create / zd_plan_create_device: the walk (host or device), then
+// the descriptors, the workspace and the upload.
+static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint32_t flags, hipStream_t s,
+                       zd_plan** out) {
   zd_plan* P = new (std::nothrow) zd_plan();
   if (!P) return ZD_E_NO_MEMORY;
   P->flags = flags;
   const auto t0 = std::chrono::steady_clock::now();
-  plan_index(P, src, n);
+  if (d_src) {
+    if (int r = plan_index_dev(P, d_src, n, s)) { zd_plan_destroy(P); return r; }
+  } else {
+    plan_index(P, src, n);
+  }
   const auto ti = std::chrono::steady_clock::now();
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {1, 4, 8};
@@ -1304,6 +1192,17 @@ int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) 
   P->info.device_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
   *out = P;
   return ZD_OK;
+}
+
+int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) {
+  if (!out || (!src && n)) return ZD_E_INVALID_ARG;
+  return plan_create(src, nullptr, n, flags, nullptr, out);
+}
+
+int zd_plan_create_device(const uint8_t* d_src, size_t n, uint32_t flags, void* stream, zd_plan** out) {
+  if (!out || (!d_src && n)) return ZD_E_INVALID_ARG;
+  static const uint8_t none = 0;
+  return plan_create(nullptr, d_src ? d_src : &none, n, flags, (hipStream_t)stream, out);
 }
 
 int zd_plan_info_get(const zd_plan* P, zd_plan_info* info) {
@@ -1693,7 +1592,7 @@ int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consume
     const uint8_t* s;
     if (int r = in.slice(hb.size, &s)) return r;
     hb.cb.src = 3; hb.cb.size = hb.size; hb.cb.host_stage = PS_ALL;
-    Err e;
+    WalkErr e;
     if (int r = parse_compressed(src, 3, hb.size, &hb.cb, &e)) return r;
   } else return ZD_E_RESERVED_BLOCK_TYPE;
   size_t used = n - in.n;

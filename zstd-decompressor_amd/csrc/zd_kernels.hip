@@ -19,6 +19,7 @@
 #include "../../include/zd.h"
 #include "zd_common.h"
 #include "zd_launch.h"
+#include "zd_walk.h"
 
 namespace zd {
 
@@ -1692,11 +1693,29 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
             ll_code(llc, &llbase, &llb);
             ml_code(mlc, &mlbase, &mlb);
 #endif
+#ifdef ZD_K4_V32
+            // the extra bits of a sequence usually fit the 32 bits below its
+            // position: three bit-field extracts on one funnel-shifted dword
+            // instead of 64-bit shifts; a batch with a wider lane takes the
+            // 64-bit path
+            const uint32_t E = ofc + mlb + llb;
+            if (__ballot(E > 32) == 0) {
+              const uint32_t k = winA.sh;              // top 32 bits below pos
+              const uint32_t hi = (uint32_t)(winA.w1 >> 32), lo = (uint32_t)winA.w1;
+              const uint32_t t32 = k == 0 ? hi : __builtin_amdgcn_alignbit(hi, lo, 32 - k);
+              const uint32_t o1 = 32 - ofc, o2 = o1 - mlb, o3 = o2 - llb;
+              ofv = (1u << ofc) + __builtin_amdgcn_ubfe(t32, o1, ofc);
+              ml = mlbase + __builtin_amdgcn_ubfe(t32, o2, mlb);
+              ll = llbase + __builtin_amdgcn_ubfe(t32, o3, llb);
+            } else
+#endif
+            {
             uint64_t t = winu_top(winA, 0);
             const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
             ofv = (1u << ofc) + ob;
             ml = mlbase + mb;
             ll = llbase + lb;
+            }
           }
         }
         K4P(0);
@@ -1805,10 +1824,20 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         if (act && ll) {
 #endif
           l_u8* d = X.at(X.pos + (int32_t)opos);
+#ifdef ZD_K4_LITSPLIT
+          // lit_stage is uniform: one loop per source kind, no per-piece select
+          if (!lit_stage) {
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, f4, ll - x);
+          } else if (lpos + ll <= K4_STG) {
+            const l_u8* sp = (const l_u8*)stg + lpos;
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lds16(sp + x), ll - x);
+          } else {
+#else
           if (!lit_stage || lpos + ll <= K4_STG) {
             const l_u8* sp = (const l_u8*)stg + lpos;
             for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
           } else {
+#endif
             for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
           }
         }
@@ -3540,6 +3569,140 @@ hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* 
                           const uint64_t* d_len, uint32_t n, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(zd_k_compact, dim3(n), dim3(256), 0, s, staging, dst, d_from, d_to, d_len);
+  return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// Device header walk: the frame / block header walk of the host
+// planner (zd_host.cpp plan_index) for an input resident in HBM, with the
+// same code (zd_walk.h index_frame: Frame::parse / Header::parse /
+// Block::parse, frame.rs:61-230, block.rs:43-72, and the fixed-size parts of
+// LiteralsSection::parse / Sequences::parse, literals.rs:88-206,
+// sequences.rs:52-143).  One wave per byte range [lo, hi): a range other than
+// the first finds its first frame magic number (64 lanes x 16 positions per
+// step), then lane 0 walks the chain of frames that start inside the range; a
+// candidate whose frame fails at once was a magic number inside data and the
+// scan goes on after it (the host walk's rule).  Count pass: the range's
+// summary (WalkRange); fill pass: its frames and blocks at f_off / b_off
+// (block indices global, so all ranges share one block array).
+// ---------------------------------------------------------------------------
+struct WalkCount {
+  uint32_t n = 0;
+  __device__ size_t size() const { return n; }
+  __device__ void push(const HostBlock&) { n++; }
+};
+struct WalkFill {
+  HostBlock* out;
+  uint64_t base;
+  uint32_t n = 0;
+  __device__ size_t size() const { return base + n; }
+  __device__ void push(const HostBlock& b) { out[base + n++] = b; }
+};
+
+// First position q in [p, hi) with a frame magic number at src[q..q+4)
+// (q + 4 <= n), else hi.  Whole wave.
+__device__ uint64_t walk_scan(const uint8_t* __restrict__ src, uint64_t n, uint64_t p, uint64_t hi, int lane) {
+  for (uint64_t base = p; base < hi; base += 1024) {
+    const uint64_t q0 = base + 16 * (uint64_t)lane;
+    uint32_t found = 16;
+    if (q0 < hi) {
+      uint8_t b[20];
+      if (q0 + 20 <= n) {
+        const u32x4a1 v = *(const u32x4a1*)(src + q0);
+        const uint32_t w = *(const uint32_t __attribute__((aligned(1)))*)(src + q0 + 16);
+        const uint32_t d[5] = {v.x, v.y, v.z, v.w, w};
+#pragma unroll
+        for (int i = 0; i < 20; i++) b[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
+      } else {
+        for (int i = 0; i < 20; i++) b[i] = q0 + i < n ? src[q0 + i] : 0;
+      }
+      for (uint32_t j = 0; j < 16; j++) {
+        const uint64_t q = q0 + j;
+        if (q >= hi) break;
+        if (q + 4 <= n && magic_word(b[j] | (uint32_t)b[j + 1] << 8 | (uint32_t)b[j + 2] << 16 | (uint32_t)b[j + 3] << 24)) {
+          found = j;
+          break;
+        }
+      }
+    }
+    const uint64_t m = __ballot(found < 16);
+    if (m) {
+      const int l = __ffsll((long long)m) - 1;
+      const uint32_t fj = (uint32_t)__shfl((int)found, l, 64);
+      return base + 16 * (uint64_t)l + fj;
+    }
+  }
+  return hi;
+}
+
+template <bool FILL>
+__global__ __launch_bounds__(64) void zd_k_walk(const uint8_t* __restrict__ src, uint64_t n, uint64_t first,
+                                               uint64_t chunk, uint32_t nranges, WalkRange* wr,
+                                               HostFrame* frames, HostBlock* blocks) {
+  const uint32_t k = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (k >= nranges) return;
+  const uint64_t lo = first + (uint64_t)k * chunk;
+  const uint64_t hi = lo + chunk < n ? lo + chunk : n;
+  if (FILL) {
+    if (lane) return;
+    WalkRange R = wr[k];
+    if (!R.nframes) return;
+    Bytes in{src + R.p0, n - R.p0};
+    WalkFill sink{blocks, R.b_off};
+    for (uint32_t f = 0; f < R.nframes; f++) {
+      HostFrame hf;
+      index_frame(src, in, &hf, sink);
+      frames[R.f_off + f] = hf;
+    }
+    return;
+  }
+  uint64_t p = lo;
+  for (;;) {
+    if (k) {
+      p = walk_scan(src, n, p, hi, lane);
+      if (p >= hi) break;
+    }
+    uint32_t nf = 0, nb = 0;
+    int st = 0;
+    uint64_t end = 0;
+    if (lane == 0) {
+      Bytes in{src + p, n - p};
+      WalkCount sink;
+      while (in.n && (uint64_t)(in.p - src) < hi) {
+        HostFrame hf;
+        const int r = index_frame(src, in, &hf, sink);
+        nf++;
+        if (r) { st = r; break; }
+      }
+      nb = sink.n;
+      end = (uint64_t)(in.p - src);
+    }
+    st = __shfl(st, 0, 64);
+    nf = (uint32_t)__shfl((int)nf, 0, 64);
+    if (k && st && nf == 1) { p++; continue; }       // a magic number inside data: look further
+    if (lane == 0) {
+      WalkRange R{};
+      R.p0 = p; R.end = end; R.nframes = nf; R.nblocks = nb; R.status = st;
+      wr[k] = R;
+    }
+    return;
+  }
+  if (lane == 0) {
+    WalkRange R{};
+    R.p0 = hi; R.end = hi;
+    wr[k] = R;
+  }
+}
+
+hipError_t launch_walk(const uint8_t* src, uint64_t n, uint64_t first, uint64_t chunk, uint32_t nranges, WalkRange* wr,
+                       HostFrame* frames, HostBlock* blocks, bool fill, hipStream_t s) {
+  if (!nranges) return hipSuccess;
+  if (fill)
+    hipLaunchKernelGGL(zd_k_walk<true>, dim3(nranges), dim3(64), 0, s, src, n, first, chunk, nranges, wr, frames, blocks);
+  else
+    hipLaunchKernelGGL(zd_k_walk<false>, dim3(nranges), dim3(64), 0, s, src, n, first, chunk, nranges, wr, frames, blocks);
   return hipGetLastError();
 }
 

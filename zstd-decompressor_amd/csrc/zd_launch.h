@@ -40,6 +40,15 @@ hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* 
 hipError_t launch_xxh64(const uint8_t* base, const uint64_t* d_off, const uint64_t* d_len, uint32_t n,
                         uint64_t* d_hash, hipStream_t s);
 
+// Device header walk (zd_walk.h): ranges [first + k chunk, + chunk) of src[0, n),
+// count pass (fill = false: WalkRange summaries) or fill pass (frames/blocks at
+// the summaries' f_off / b_off).
+struct WalkRange;
+struct HostFrame;
+struct HostBlock;
+hipError_t launch_walk(const uint8_t* src, uint64_t n, uint64_t first, uint64_t chunk, uint32_t nranges, WalkRange* wr,
+                       HostFrame* frames, HostBlock* blocks, bool fill, hipStream_t s);
+
 constexpr int N_KERNELS = 6;
 constexpr uint32_t K4F_CAP = 128u << 10;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];

@@ -61,6 +61,7 @@ SIGNATURES = {
     "zd_trim_cache": (None, []),
     "zd_frames_index": (C.c_int, [_vp, _sz, C.POINTER(FrameDesc), _sz, _szp, C.POINTER(BlockDesc), _sz, _szp, _szp]),
     "zd_plan_create": (C.c_int, [_vp, _sz, C.c_uint32, C.POINTER(_vp)]),
+    "zd_plan_create_device": (C.c_int, [_vp, _sz, C.c_uint32, _vp, C.POINTER(_vp)]),
     "zd_plan_info_get": (C.c_int, [_vp, C.POINTER(PlanInfo)]),
     "zd_plan_destroy": (None, [_vp]),
     "zd_decode_async": (C.c_int, [_vp, _vp, _vp, _sz, _vp]),

@@ -71,6 +71,21 @@ class Plan:
         self.info = PlanInfo()
         _lib.check(L.zd_plan_info_get(h, C.byref(self.info)), "zd_plan_info_get")
 
+    @classmethod
+    def from_device(cls, d_src: int, n: int, print_skippable: bool = False, flags: int = 0, stream: int = 0):
+        """zd_plan_create_device: the same plan for n bytes resident in HBM at d_src
+        (readable for n + 16 bytes); the frame/block header walk runs on the GPU."""
+        self = cls.__new__(cls)
+        L = _lib.lib()
+        self._data, self._keep = None, None
+        h = C.c_void_p()
+        _lib.check(L.zd_plan_create_device(C.c_void_p(d_src), n, (_lib.F_SKIPPABLE if print_skippable else 0) | flags,
+                                           C.c_void_p(stream), C.byref(h)), "zd_plan_create_device")
+        self._h = h
+        self.info = PlanInfo()
+        _lib.check(L.zd_plan_info_get(h, C.byref(self.info)), "zd_plan_info_get")
+        return self
+
     def set_profiling(self, on: bool = True):
         _lib.check(_lib.lib().zd_plan_set_profiling(self._h, int(on)))
 
