@@ -1207,6 +1207,190 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
   if (st) k3_fail(C, ci, cstate, fstate, st);
 }
 // ---------------------------------------------------------------------------
+// K3Q: the fast chain with four lanes per block (a quad): lane roles OF, ML,
+// LL and a dummy, each with its own table, state and bit count, so a step is
+// one table lookup per lane instead of three per lane; the three counts are
+// summed and the state bits split with quad DPP moves, the window select is
+// the same in all four lanes.  Records, checks and the exact-chain fallback
+// are seq_chainfl's (same records bit for bit).  The fourth lane shadows the
+// LL lane (its table, its states stay valid indices) and is masked out of
+// the sums, the bit split and the record (LDS is full: no room for a dummy
+// table next to four workgroups' 40 KiB of tables).
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ inline uint32_t qdpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+constexpr int QP_SWAP1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int QP_SWAP2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int QP_SHR1 = 0x90;    // quad_perm [0,0,1,2]
+constexpr int QP_L1TO2 = 0x10;   // quad_perm [0,0,1,0]
+__device__ inline uint32_t quad_sum(uint32_t x) {
+  x += qdpp<QP_SWAP1>(x);
+  return x + qdpp<QP_SWAP2>(x);
+}
+__device__ inline uint32_t quad_or(uint32_t x) {
+  x |= qdpp<QP_SWAP1>(x);
+  return x | qdpp<QP_SWAP2>(x);
+}
+__device__ inline uint32_t quad_max(uint32_t x) {
+  x = max(x, qdpp<QP_SWAP1>(x));
+  return max(x, qdpp<QP_SWAP2>(x));
+}
+// exclusive prefix over roles 0, 1, 2 (m0: 0 in role 0, else all ones)
+__device__ inline uint32_t quad_excl(uint32_t x, uint32_t m0) {
+  const uint32_t t = qdpp<QP_SHR1>(x) & m0;
+  return t + qdpp<QP_L1TO2>(t);
+}
+
+template <int L, int N>
+__device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
+                          int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
+  constexpr int U = (L % 2 == 0) ? L : 2 * L;
+  if (bs_size == 0) return 1;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return 1;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);
+  const int32_t A = all + alo + alm;
+  if (A > pos) return 1;
+  if ((intptr_t)bs - (intptr_t)base + (intptr_t)bs_size < 4 * N) return 1;
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)(-4 * N));
+  const int32_t pos0 = pos;
+  const Win6 wi = win6_load(bs, m, pos);
+  const uint32_t v0 = win6_bits(wi, pos, (uint32_t)A);
+  // this lane's role: OF (0) | ML (1) | LL (2) | LL's shadow (3, masked by m3)
+  const int alr = role == 0 ? alo : role == 1 ? alm : all;
+  const uint32_t m3 = role == 3 ? 0u : ~0u, m0 = role == 0 ? 0u : ~0u;
+  const uint32_t ar = (uint32_t)(alr - 31), Tr = 1u << alr;
+  const uint32_t shr = role == 0 ? 20 : role == 1 ? 10 : 0;
+  uint32_t s = role == 0 ? __builtin_amdgcn_ubfe(v0, alm, alo)
+             : role == 1 ? __builtin_amdgcn_ubfe(v0, 0, alm)
+             : v0 >> (alo + alm);
+  pos -= A;
+  typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(8)));
+  const uint64_t r0 = (uint64_t)(uint32_t)pos | ((uint64_t)quad_or((s << shr) & m3) << 32);
+  const bool writer = role == 0;
+  WinN<N> w[L];
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    w[k] = winn_load<N>(bs, m, k == 0 ? pos0 : pos);
+    if (k & 1) {
+      asm volatile("" ::: "memory");
+      if (writer) *(u64x2u*)out = u64x2u{r0, r0};
+    }
+  }
+  if (L & 1) {
+    asm volatile("" ::: "memory");
+    if (writer) *(u64x2u*)out = u64x2u{r0, r0};
+  }
+  uint32_t mx = 0;
+  int32_t ymin = 0;
+  auto step = [&](WinN<N>& use) -> uint64_t {
+    const uint32_t e = tab[s];
+    mx = max(mx, e & m3);
+    const uint32_t ns = e & 1023, nb = __builtin_clz(ns) + ar;
+    pos -= (int32_t)quad_sum((e >> 10) & m3);
+    const int32_t y = pos - use.wb;
+    ymin = min(ymin, y);
+    const uint32_t r = winn_at<N>(use, (uint32_t)y);
+    use = winn_load<N>(bs, m, pos);
+    const uint32_t v = __builtin_amdgcn_ubfe(r, quad_excl(nb, m0), nb);
+    s = (ns << nb) + v - Tr;
+    return (uint64_t)(uint32_t)pos | ((uint64_t)quad_or((s << shr) & m3) << 32);
+  };
+  for (uint32_t i = 0; i + 1 < n; i += U) {
+#pragma unroll
+    for (int k = 0; k < U; k += 2) {
+      const uint64_t qa = step(w[k % L]);
+      const uint64_t qb = step(w[(k + 1) % L]);
+      asm volatile("" ::: "memory");
+      const uint32_t slot = i + 1 + k;
+      if (writer) *(u64x2u*)(out + (slot < n ? slot : n)) = u64x2u{qa, qb};
+    }
+  }
+  const uint64_t rl = *(volatile uint64_t*)(out + n - 1);
+  const int32_t pl = (int32_t)(uint32_t)rl;
+  const uint32_t st = (uint32_t)(rl >> 32);
+  const uint32_t el = tab[(st >> shr) & 1023] & m3;
+  mx = quad_max(max(mx, el));
+  const uint32_t S = quad_sum((__builtin_clz(el & 1023) + ar) & m3);
+  const int32_t E = (int32_t)(quad_sum(el >> 10) - S);
+  return (mx >= K3F_BAD || ymin < 0 || pl < 0 || E > pl) ? 1 : 0;
+}
+
+constexpr int K3Q_CHAINS = 16;          // blocks per workgroup (one wave, four lanes each)
+__global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict__ src,
+                                                       const CompBlock* __restrict__ comp, CompState* cstate,
+                                                       FrameState* fstate, const uint32_t* __restrict__ list,
+                                                       uint32_t n_list, const uint16_t* __restrict__ fses,
+                                                       uint64_t* __restrict__ recs) {
+  __shared__ __attribute__((aligned(16))) uint16_t tabs[K3Q_CHAINS * K3_TAB];
+  const int lane = threadIdx.x;
+  const int role = lane & 3, q = lane >> 2;
+  const uint32_t li = blockIdx.x * K3Q_CHAINS + q;
+  bool act = li < n_list;
+  const uint32_t ci = act ? list[li] : 0;
+  CompBlock C;
+  if (act) C = comp[ci];
+  if (act) {
+    const uint64_t key0 = fstate[C.frame].key;
+    if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) act = false;
+  }
+  int al[3] = {0, 0, 0};
+  const uint16_t* g[3] = {nullptr, nullptr, nullptr};
+  if (act) {
+    for (int k = 0; k < 3; k++) {
+      const uint32_t sidx = (uint32_t)C.tab_src[k];
+      al[k] = cstate[sidx].al[k];
+      g[k] = fses + (uint64_t)comp[sidx].fse_slot * FSE_SLOT + k * FSE_TAB;
+    }
+  }
+  const bool deep = act && al[1] > 8;
+  const bool use_lds = __ballot(deep) == 0;
+  lds_u16* mine = (lds_u16*)tabs + q * K3_TAB;
+  if (use_lds && act) {
+    // the quad's lanes fill the three tables (lane k < 3: table k)
+    const int dst[3] = {0, K3_TL + K3_TM, K3_TL};     // LL | ML | OF in LDS
+    if (role < 3) {
+      const int k = role;
+      const int cnt = 1 << al[k];
+      if (cnt >= 8) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const u32x4 g_u4;
+        typedef __attribute__((address_space(3))) u32x4 l_u4;
+        g_u4* s4 = (g_u4*)g[k];
+        l_u4* d4 = (l_u4*)(mine + dst[k]);
+        for (int e = 0; e < cnt / 8; e++) {
+          u32x4 v = s4[e];
+          v.x = K3_ENTRY(v.x & 0xFFFF, k, al[k]) | (K3_ENTRY(v.x >> 16, k, al[k]) << 16);
+          v.y = K3_ENTRY(v.y & 0xFFFF, k, al[k]) | (K3_ENTRY(v.y >> 16, k, al[k]) << 16);
+          v.z = K3_ENTRY(v.z & 0xFFFF, k, al[k]) | (K3_ENTRY(v.z >> 16, k, al[k]) << 16);
+          v.w = K3_ENTRY(v.w & 0xFFFF, k, al[k]) | (K3_ENTRY(v.w >> 16, k, al[k]) << 16);
+          d4[e] = v;
+        }
+      } else {
+        for (int e = 0; e < cnt; e++) mine[dst[k] + e] = (uint16_t)K3_ENTRY(((g_u16*)g[k])[e], k, al[k]);
+      }
+    }
+  }
+  __syncthreads();
+  if (!act) return;
+  const CompState cs = cstate[ci];
+  const uint8_t* blk = src + C.src;
+  const uintptr_t lo = (uintptr_t)src;
+  int st = 0;
+  bool exact = !use_lds;
+  if (use_lds) {
+    const lds_u16* tab = role == 0 ? mine + K3_TL + K3_TM : role == 1 ? mine + K3_TL : mine;
+    exact = seq_chainq<ZD_K3_LA, ZD_K3_WN>(blk + cs.bs_off, cs.bs_size, lo, tab, role, al[0], al[1], al[2], C.nseq,
+                                          recs + C.seq_out) != 0;
+  }
+  if (exact && role == 0)
+    st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0],
+                                 al[1], al[2], C.nseq, recs + C.seq_out);
+  if (st) k3_fail(C, ci, cstate, fstate, st);
+}
+// ---------------------------------------------------------------------------
 // K4: execute (decoding_context.rs:50-106 + block.rs:74-99), one frame per
 // wave, one sequence per lane, 64 sequences per batch.  A frame that decodes
 // past the capacity its plan reserved (its Frame_Content_Size, or 128 KiB per
@@ -3506,9 +3690,15 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   auto k3 = [&](uint32_t l0, uint32_t l1) {
     if (l1 > l0 && (a.kmask & 4))
+#ifdef ZD_K3_QUAD
+      hipLaunchKernelGGL(zd_k_sequences_q, dim3((l1 - l0 + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, s, a.src, comp,
+                         cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0, (const uint16_t*)fses,
+                         seqs);
+#else
       hipLaunchKernelGGL(zd_k_sequences, dim3((l1 - l0 + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
                          cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0, (const uint16_t*)fses,
                          seqs);
+#endif
   };
   auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st) {
     const uint32_t n = f1 - f0;
