@@ -256,6 +256,26 @@ def test_many_frame_roundtrip_large():
     assert decompress(data) == src
 
 
+def test_one_round_plan():
+    """A plan of 3,000 frames of 8 KiB (one round of K3 chains and of K2
+    blocks, like one rank's share of C4 on 8 GPUs): round trip, then
+    corruptions inside the plan against the oracle."""
+    r = random.Random(78)
+    src = gen.text(3000 * 8192, seed=14)
+    base = gen.frames(src, 8192, 3)
+    from zstd_decompressor import decompress
+    from zstd_decompressor.batch import frames_index
+    assert decompress(base) == src
+    spans = [(f["src_offset"], f["src_size"]) for f in frames_index(base)[0]]
+    assert len(spans) == 3000
+    for it in range(8):
+        d = bytearray(base)
+        o, n = spans[r.randrange(100, 2900)]
+        for _ in range(r.randrange(1, 4)):
+            d[o + r.randrange(n)] = r.randrange(256)
+        assert_parity(bytes(d), False, f"per-CU plan corrupt #{it}", allow_ood=True)
+
+
 def _ncount(al, probs):
     """FSE table description (the inverse of parse_fse_table, fse.rs:16-69):
     probabilities of symbols 0.. (-1 = "less than one"), LSB-first bits."""

@@ -3800,7 +3800,8 @@ __device__ uint64_t walk_scan(const uint8_t* __restrict__ src, uint64_t n, uint6
       uint8_t b[20];
       if (q0 + 20 <= n) {
         const u32x4a1 v = *(const u32x4a1*)(src + q0);
-        const uint32_t w = *(const uint32_t __attribute__((aligned(1)))*)(src + q0 + 16);
+        typedef uint32_t u32a1 __attribute__((aligned(1)));
+        const uint32_t w = *(const u32a1*)(src + q0 + 16);
         const uint32_t d[5] = {v.x, v.y, v.z, v.w, w};
 #pragma unroll
         for (int i = 0; i < 20; i++) b[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
