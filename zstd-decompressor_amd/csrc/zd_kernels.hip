@@ -3791,37 +3791,48 @@ struct WalkFill {
 };
 
 // First position q in [p, hi) with a frame magic number at src[q..q+4)
-// (q + 4 <= n), else hi.  Whole wave.
+// (q + 4 <= n), else hi.  Whole wave, 4 KiB a step: each lane checks 64
+// positions from 68 loaded bytes (four 16-byte loads in flight), a
+// position's word is one alignbyte of two loaded dwords.  (1 KiB steps of
+// 16 positions per lane took ~11 us each: latency-bound.)
 __device__ uint64_t walk_scan(const uint8_t* __restrict__ src, uint64_t n, uint64_t p, uint64_t hi, int lane) {
-  for (uint64_t base = p; base < hi; base += 1024) {
-    const uint64_t q0 = base + 16 * (uint64_t)lane;
-    uint32_t found = 16;
+  typedef uint32_t u32a1 __attribute__((aligned(1)));
+  for (uint64_t base = p; base < hi; base += 4096) {
+    const uint64_t q0 = base + 64 * (uint64_t)lane;
+    uint64_t hit = 0;                            // bit j: a magic number at q0 + j
     if (q0 < hi) {
-      uint8_t b[20];
-      if (q0 + 20 <= n) {
-        const u32x4a1 v = *(const u32x4a1*)(src + q0);
-        typedef uint32_t u32a1 __attribute__((aligned(1)));
-        const uint32_t w = *(const u32a1*)(src + q0 + 16);
-        const uint32_t d[5] = {v.x, v.y, v.z, v.w, w};
+      uint32_t d[17];
+      if (q0 + 68 <= n) {
 #pragma unroll
-        for (int i = 0; i < 20; i++) b[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
+        for (int i = 0; i < 4; i++) {
+          const u32x4a1 v = *(const u32x4a1*)(src + q0 + 16 * i);
+          d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+        }
+        d[16] = *(const u32a1*)(src + q0 + 64);
       } else {
-        for (int i = 0; i < 20; i++) b[i] = q0 + i < n ? src[q0 + i] : 0;
-      }
-      for (uint32_t j = 0; j < 16; j++) {
-        const uint64_t q = q0 + j;
-        if (q >= hi) break;
-        if (q + 4 <= n && magic_word(b[j] | (uint32_t)b[j + 1] << 8 | (uint32_t)b[j + 2] << 16 | (uint32_t)b[j + 3] << 24)) {
-          found = j;
-          break;
+        for (int i = 0; i < 17; i++) {
+          uint32_t w = 0;
+          for (int b = 0; b < 4; b++) {
+            const uint64_t q = q0 + 4 * i + b;
+            w |= (uint32_t)(q < n ? src[q] : 0) << (8 * b);
+          }
+          d[i] = w;
         }
       }
+#pragma unroll
+      for (int j = 0; j < 64; j++) {
+        const uint32_t m = __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3);
+        hit |= (uint64_t)magic_word(m) << j;
+      }
+      // positions at or past hi, or whose word runs past n, do not count
+      const uint64_t lim = min(hi, n >= 3 ? n - 3 : 0);
+      if (q0 + 64 > lim) hit &= lim > q0 ? ((1ull << (lim - q0)) - 1) : 0;
     }
-    const uint64_t m = __ballot(found < 16);
+    const uint64_t m = __ballot(hit != 0);
     if (m) {
       const int l = __ffsll((long long)m) - 1;
-      const uint32_t fj = (uint32_t)__shfl((int)found, l, 64);
-      return base + 16 * (uint64_t)l + fj;
+      const uint32_t fj = (uint32_t)__shfl((int)(hit ? __ffsll((long long)hit) - 1 : 0), l, 64);
+      return base + 64 * (uint64_t)l + fj;
     }
   }
   return hi;
@@ -3850,9 +3861,16 @@ __global__ __launch_bounds__(64) void zd_k_walk(const uint8_t* __restrict__ src,
     return;
   }
   uint64_t p = lo;
+#ifdef ZD_WALK_PROF
+  uint64_t t_scan = 0, t_walk = 0, t0 = __builtin_amdgcn_s_memtime();
+  uint32_t tries = 0;
+#endif
   for (;;) {
     if (k) {
       p = walk_scan(src, n, p, hi, lane);
+#ifdef ZD_WALK_PROF
+      t_scan += __builtin_amdgcn_s_memtime() - t0; t0 = __builtin_amdgcn_s_memtime(); tries++;
+#endif
       if (p >= hi) break;
     }
     uint32_t nf = 0, nb = 0;
@@ -3872,6 +3890,13 @@ __global__ __launch_bounds__(64) void zd_k_walk(const uint8_t* __restrict__ src,
     }
     st = __shfl(st, 0, 64);
     nf = (uint32_t)__shfl((int)nf, 0, 64);
+#ifdef ZD_WALK_PROF
+    t_walk += __builtin_amdgcn_s_memtime() - t0; t0 = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && (k == 1 || k == 100 || k == 1000 || k == 5000))
+      printf("walk range %u: lo %llu p %llu scan %llu walk %llu cycles, tries %u, frames %u\n", k,
+             (unsigned long long)lo, (unsigned long long)p, (unsigned long long)t_scan, (unsigned long long)t_walk,
+             tries, nf);
+#endif
     if (k && st && nf == 1) { p++; continue; }       // a magic number inside data: look further
     if (lane == 0) {
       WalkRange R{};
