@@ -223,6 +223,9 @@ int zd_plan_checksums(zd_plan* plan, const uint8_t* d_dst, void* stream, int32_t
 int zd_plan_set_profiling(zd_plan* plan, int enable);
 int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, int* n);
 
+/* zd_decompress with a plan already made for the same n bytes (so a caller
+ * that sized dst from zd_plan_info_get does not plan twice). */
+int zd_plan_decompress(zd_plan* plan, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 /* Convenience: host in, host out (H2D + decode + D2H on the default
  * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
 int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,

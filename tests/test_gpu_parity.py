@@ -256,6 +256,26 @@ def test_many_frame_roundtrip_large():
     assert decompress(data) == src
 
 
+def test_plan_decompress_reuses_the_plan(resources):
+    """zd_plan_decompress: host in / host out with a plan made once (the
+    INTEGRATION.md decompress() pattern), equal to the oracle's output."""
+    import ctypes as C
+    from zstd_decompressor import _lib
+    from zstd_decompressor.batch import Plan
+    L = _lib.lib()
+    for name, data in resources.items():
+        ost, oout = oracle.decompress_status(data)
+        plan = Plan(data)
+        cap = max(plan.info.out_bytes, 1)
+        buf = (C.c_uint8 * cap)()
+        n = C.c_size_t()
+        p, nb, keep = _lib.buf(data)
+        st = L.zd_plan_decompress(plan._h, p, nb, buf, cap, C.byref(n))
+        assert st == ost, name
+        assert bytes(buf[: n.value]) == oout, name
+        plan.close()
+
+
 def test_one_round_plan():
     """A plan of 3,000 frames of 8 KiB (one round of K3 chains and of K2
     blocks, like one rank's share of C4 on 8 GPUs): round trip, then

@@ -992,6 +992,8 @@ int plan_index_dev(zd_plan* P, const uint8_t* d_src, size_t n, hipStream_t s) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (B.dev != dev) {                      // buffers of another device: start over
+      if (B.d_wr) (void)hipFree(B.d_wr);
+      if (B.d_out) (void)hipFree(B.d_out);
       B.d_wr = nullptr; B.cap_wr = 0; B.d_out = nullptr; B.cap_out = 0;
       B.dev = dev;
     }
@@ -1403,18 +1405,16 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
   return ZD_OK;
 }
 
-int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, uint32_t flags) {
-  zd_plan* P = nullptr;
-  int r = zd_plan_create(src, n, flags, &P);
-  if (r) return r;
+int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+  if (!P || (!src && n) || n != P->info.src_bytes) return ZD_E_INVALID_ARG;
   uint8_t *d_src = nullptr, *d_dst = nullptr;
   uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
-  auto cleanup = [&]() { if (d_src) (void)hipFree(d_src); if (d_dst) (void)hipFree(d_dst); zd_plan_destroy(P); };
+  auto cleanup = [&]() { if (d_src) (void)hipFree(d_src); if (d_dst) (void)hipFree(d_dst); };
   if (hipMalloc(&d_src, n + ZD_SRC_PADDING) != hipSuccess || hipMalloc(&d_dst, ob) != hipSuccess) {
     cleanup(); return ZD_E_HIP;
   }
   if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) { cleanup(); return ZD_E_HIP; }
-  r = zd_decode_async(P, d_src, d_dst, ob, nullptr);
+  int r = zd_decode_async(P, d_src, d_dst, ob, nullptr);
   uint64_t total = 0;
   int32_t first = -1;
   if (!r) r = zd_plan_results(P, d_dst, nullptr, nullptr, nullptr, &total, &first);
@@ -1426,6 +1426,15 @@ int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t
   cleanup();
   if (!status && total > cap) return ZD_E_DST_TOO_SMALL;
   return status;
+}
+
+int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, uint32_t flags) {
+  zd_plan* P = nullptr;
+  int r = zd_plan_create(src, n, flags, &P);
+  if (r) return r;
+  r = zd_plan_decompress(P, src, n, dst, cap, out_len);
+  zd_plan_destroy(P);
+  return r;
 }
 
 // ===========================================================================
@@ -1446,9 +1455,28 @@ struct zd_context {
   uint8_t al[3] = {0, 0, 0};
   bool has_huf = false;
   bool has_tab[3] = {false, false, false};
+  // kept between calls: the stream every block runs on (one synchronisation
+  // per block) and the block-input buffer (grown, never freed per call)
+  hipStream_t s = nullptr;
+  uint8_t* d_in = nullptr;
+  uint64_t in_cap = 0;
 };
 
 namespace {
+
+// The caller's bytes in the context's input buffer (async on its stream).
+int ctx_input(zd_context* c, const uint8_t* src, size_t n) {
+  if (n + ZD_SRC_PADDING > c->in_cap) {
+    if (c->d_in) (void)hipFree(c->d_in);
+    c->d_in = nullptr;
+    c->in_cap = 0;
+    const uint64_t nc = std::max<uint64_t>(n + ZD_SRC_PADDING, 256u << 10);
+    HIPCHK(hipMalloc(&c->d_in, nc));
+    c->in_cap = nc;
+  }
+  if (n) HIPCHK(hipMemcpyAsync(c->d_in, src, n, hipMemcpyHostToDevice, c->s));
+  return 0;
+}
 
 int ctx_reserve(zd_context* c, uint64_t need) {
   if (need <= c->d_cap) return 0;
@@ -1472,7 +1500,8 @@ int zd_context_new(uint64_t window_size, zd_context** out) {
   zd_context* c = new (std::nothrow) zd_context();
   if (!c) return ZD_E_NO_MEMORY;
   c->window = window_size;
-  if (hipMalloc(&c->d_lut, LUT_ENTRIES * 2) != hipSuccess || hipMalloc(&c->d_fse, FSE_SLOT * 2) != hipSuccess) {
+  if (hipMalloc(&c->d_lut, LUT_ENTRIES * 2) != hipSuccess || hipMalloc(&c->d_fse, FSE_SLOT * 2) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) {
     zd_context_free(c);
     return ZD_E_HIP;
   }
@@ -1485,6 +1514,8 @@ void zd_context_free(zd_context* c) {
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_fse) (void)hipFree(c->d_fse);
+  if (c->d_in) (void)hipFree(c->d_in);
+  if (c->s) { (void)hipStreamSynchronize(c->s); (void)hipStreamDestroy(c->s); }
   delete c;
 }
 
@@ -1502,58 +1533,60 @@ int zd_context_offsets(const zd_context* c, uint64_t offsets[3]) {
   return ZD_OK;
 }
 
-// Runs a one-frame plan whose output continues the context's decoded buffer.
+// Runs a one-frame plan whose output continues the context's decoded buffer:
+// copies and kernels on the context's stream, one synchronisation (for the
+// frame state and the block's table state).
 static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
-  uint8_t* d_src = nullptr;
-  auto fin = [&](int r) { if (d_src) (void)hipFree(d_src); return r; };
-  if (hipMalloc(&d_src, n + ZD_SRC_PADDING) != hipSuccess) return ZD_E_HIP;
-  if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
-  if (int r = upload_plan(P)) return fin(r);
-  HIPCHK(hipMemset(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState)));
+  if (int r = upload_plan(P)) return r;
+  if (int r = ctx_input(c, src, n)) return r;
+  const hipStream_t s = c->s;
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
   // prebuilt comp 0 carries the context's tables
+  CompState pcs{};
   if (P->has_prebuilt) {
     const CompBlock& pb = P->comps[0];
     uint8_t* luts = P->d_ws + P->W.luts + (uint64_t)pb.lut_slot * LUT_ENTRIES * 2;
     uint8_t* fses = P->d_ws + P->W.fses + (uint64_t)pb.fse_slot * FSE_SLOT * 2;
-    if (hipMemcpy(luts, c->d_lut, LUT_ENTRIES * 2, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
-    if (hipMemcpy(fses, c->d_fse, FSE_SLOT * 2, hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
-    CompState cs{};
-    cs.huf_bits = c->huf_bits;
-    for (int k = 0; k < 3; k++) cs.al[k] = c->al[k];
-    if (hipMemcpy(P->d_ws + P->W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+    HIPCHK(hipMemcpyAsync(luts, c->d_lut, LUT_ENTRIES * 2, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(fses, c->d_fse, FSE_SLOT * 2, hipMemcpyDeviceToDevice, s));
+    pcs.huf_bits = c->huf_bits;
+    for (int k = 0; k < 3; k++) pcs.al[k] = c->al[k];
+    HIPCHK(hipMemcpyAsync(P->d_ws + P->W.comp_state, &pcs, sizeof pcs, hipMemcpyHostToDevice, s));
   }
   P->info.out_exact = 1;    // output goes straight into the context buffer
   P->fdesc[0].out = 0;
-  if (hipMemcpy(P->d_ws + P->W.frames, P->fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice) != hipSuccess)
-    return fin(ZD_E_HIP);
-  HIPCHK(hipMemcpy(P->d_ws + P->W.frame_state, P->fstate0.data(), sizeof(FrameState), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frames, P->fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->fstate0.data(), sizeof(FrameState), hipMemcpyHostToDevice, s));
   LaunchArgs a{};
-  a.src = d_src; a.src_size = n; a.out = c->d_out; a.ws = P->d_ws; a.W = P->W;
+  a.src = c->d_in; a.src_size = n; a.out = c->d_out; a.ws = P->d_ws; a.W = P->W;
   a.n_tables = (uint32_t)P->list_tables.size();
   a.n_huf = (uint32_t)P->list_huf.size();
   a.n_seq = (uint32_t)P->list_seq.size();
   a.n_frames = 1;
   a.n_k4f = (uint32_t)P->list_k4f.size();
   a.n_copies = (uint32_t)P->copies.size();
-  a.stream = nullptr;
-  if (launch_pipeline(a) != hipSuccess) return fin(ZD_E_HIP);
-  if (hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
+  a.stream = s;
+  if (launch_pipeline(a) != hipSuccess) return ZD_E_HIP;
+  // the frame state and every block's table state in one synchronisation
+  const size_t nc = P->comps.size();
+  std::vector<CompState> cst(std::max<size_t>(nc, 1));
   FrameState st{};
-  if (hipMemcpy(&st, P->d_ws + P->W.frame_state, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return fin(ZD_E_HIP);
+  HIPCHK(hipMemcpyAsync(&st, P->d_ws + P->W.frame_state, sizeof st, hipMemcpyDeviceToHost, s));
+  if (nc) HIPCHK(hipMemcpyAsync(cst.data(), P->d_ws + P->W.comp_state, nc * sizeof(CompState), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
   int code = key_code(st.key);
-  if (code) return fin(code);
+  if (code) return code;
   c->len = st.out_len;
   for (int i = 0; i < 3; i++) c->rep[i] = st.rep[i];
-  // persist tables defined by the real block (comp index 1 when prebuilt, else 0)
+  // persist tables defined by the real block (comp index 1 when prebuilt, else 0);
+  // the device copies stay on the stream, ahead of the next block's work
   size_t ci = P->has_prebuilt ? 1 : 0;
-  if (ci < P->comps.size()) {
+  if (ci < nc) {
     const CompBlock& cb = P->comps[ci];
-    CompState cs{};
-    if (hipMemcpy(&cs, P->d_ws + P->W.comp_state + ci * sizeof(CompState), sizeof cs, hipMemcpyDeviceToHost) != hipSuccess)
-      return fin(ZD_E_HIP);
+    const CompState& cs = cst[ci];
     if (cb.lit_type == LIT_COMPRESSED) {
-      if (hipMemcpy(c->d_lut, P->d_ws + P->W.luts + (uint64_t)cb.lut_slot * LUT_ENTRIES * 2, LUT_ENTRIES * 2,
-                    hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
+      HIPCHK(hipMemcpyAsync(c->d_lut, P->d_ws + P->W.luts + (uint64_t)cb.lut_slot * LUT_ENTRIES * 2, LUT_ENTRIES * 2,
+                            hipMemcpyDeviceToDevice, s));
       c->huf_bits = cs.huf_bits;
       c->has_huf = true;
     }
@@ -1561,19 +1594,18 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
       int32_t srcc = cb.tab_src[k];
       if (srcc < 0) continue;
       const CompBlock& sb = P->comps[(size_t)srcc];
-      CompState ss{};
-      if (hipMemcpy(&ss, P->d_ws + P->W.comp_state + (size_t)srcc * sizeof(CompState), sizeof ss, hipMemcpyDeviceToHost) != hipSuccess)
-        return fin(ZD_E_HIP);
       if ((size_t)srcc == ci) {
-        if (hipMemcpy(c->d_fse + k * FSE_TAB,
-                      P->d_ws + P->W.fses + ((uint64_t)sb.fse_slot * FSE_SLOT + k * FSE_TAB) * 2, FSE_TAB * 2,
-                      hipMemcpyDeviceToDevice) != hipSuccess) return fin(ZD_E_HIP);
-        c->al[k] = ss.al[k];
+        HIPCHK(hipMemcpyAsync(c->d_fse + k * FSE_TAB,
+                              P->d_ws + P->W.fses + ((uint64_t)sb.fse_slot * FSE_SLOT + k * FSE_TAB) * 2, FSE_TAB * 2,
+                              hipMemcpyDeviceToDevice, s));
+        c->al[k] = cst[(size_t)srcc].al[k];
       }
       c->has_tab[k] = true;
     }
+    // the plan's workspace is released after this call: the copies out of it first
+    HIPCHK(hipStreamSynchronize(s));
   }
-  return fin(ZD_OK);
+  return ZD_OK;
 }
 
 int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consumed, int* last) {
@@ -1725,45 +1757,46 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   P.list_huf.clear();
   P.list_seq.clear();   // sequences come from the caller
   P.info.src_bytes = nlits;
-  uint8_t* d_src = nullptr;
   int r = upload_plan(&P);
   auto fin = [&](int rr) {
-    if (d_src) (void)hipFree(d_src);
     ws_release(P.d_ws, P.ws_bytes);
     if (P.d_staging) (void)hipFree(P.d_staging);
     P.d_ws = nullptr; P.d_staging = nullptr;
     return rr;
   };
   if (r) return fin(r);
-  if (hipMalloc(&d_src, nlits + ZD_SRC_PADDING) != hipSuccess) return fin(ZD_E_HIP);
-  if (nlits && hipMemcpy(d_src, lits, nlits, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+  const hipStream_t s = c->s;
+  if (int rr = ctx_input(c, lits, nlits)) return fin(rr);
   // the caller's triples as direct records (zd_common.h); offsets are
   // exact below DIRECT_GIANT, which stays past every decoded length here
   CompState cs{};
   cs.lit_count = (uint32_t)nlits;
+  std::vector<uint64_t> rec(nseq);
   if (nseq) {
     if (need >= DIRECT_GIANT - 3) return fin(ZD_E_OUT_OF_DOMAIN);
-    std::vector<uint64_t> rec(nseq);
     for (size_t i = 0; i < nseq; i++) {
       if (ll[i] > 0x1FFFF || ml[i] > 0x3FFFF) return fin(ZD_E_OUT_OF_DOMAIN);
       rec[i] = seq_pack(ll[i], ml[i], ofv[i]);
     }
-    if (hipMemcpy(P.d_ws + P.W.seqs, rec.data(), nseq * 8, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
+    if (hipMemcpyAsync(P.d_ws + P.W.seqs, rec.data(), nseq * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+      return fin(ZD_E_HIP);
   }
-  if (hipMemcpy(P.d_ws + P.W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice) != hipSuccess) return fin(ZD_E_HIP);
   P.fdesc[0].out = 0;
-  if (hipMemcpy(P.d_ws + P.W.frames, P.fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice) != hipSuccess)
-    return fin(ZD_E_HIP);
-  if (hipMemcpy(P.d_ws + P.W.frame_state, P.fstate0.data(), sizeof(FrameState), hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpyAsync(P.d_ws + P.W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(P.d_ws + P.W.frames, P.fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(P.d_ws + P.W.frame_state, P.fstate0.data(), sizeof(FrameState), hipMemcpyHostToDevice, s) != hipSuccess)
     return fin(ZD_E_HIP);
   LaunchArgs a{};
-  a.src = d_src; a.src_size = nlits; a.out = c->d_out; a.ws = P.d_ws; a.W = P.W;
+  a.src = c->d_in; a.src_size = nlits; a.out = c->d_out; a.ws = P.d_ws; a.W = P.W;
   a.n_frames = 1;
   a.n_k4f = (uint32_t)P.list_k4f.size();
   a.n_copies = (uint32_t)P.copies.size();
-  if (launch_pipeline(a) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fin(ZD_E_HIP);
+  a.stream = s;
   FrameState st{};
-  if (hipMemcpy(&st, P.d_ws + P.W.frame_state, sizeof st, hipMemcpyDeviceToHost) != hipSuccess) return fin(ZD_E_HIP);
+  if (launch_pipeline(a) != hipSuccess ||
+      hipMemcpyAsync(&st, P.d_ws + P.W.frame_state, sizeof st, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fin(ZD_E_HIP);
   int code = key_code(st.key);
   if (code) return fin(code);
   c->len = st.out_len;

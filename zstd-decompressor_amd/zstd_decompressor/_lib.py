@@ -71,6 +71,7 @@ SIGNATURES = {
     "zd_plan_set_profiling": (C.c_int, [_vp, C.c_int]),
     "zd_plan_kernel_times": (C.c_int, [_vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)]),
     "zd_decompress": (C.c_int, [_vp, _sz, _vp, _sz, _szp, C.c_uint32]),
+    "zd_plan_decompress": (C.c_int, [_vp, _vp, _sz, _vp, _sz, _szp]),
     "zd_context_new": (C.c_int, [C.c_uint64, C.POINTER(_vp)]),
     "zd_context_free": (None, [_vp]),
     "zd_block_decode": (C.c_int, [_vp, _vp, _sz, _szp, C.POINTER(C.c_int)]),
