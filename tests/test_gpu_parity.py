@@ -256,6 +256,31 @@ def test_many_frame_roundtrip_large():
     assert decompress(data) == src
 
 
+def test_one_lane_k3_chain(resources):
+    """K3 runs four lanes per block by default (K3Q, seq_chainq); ZD_K3Q=0
+    keeps the one-lane chain (seq_chainfl).  Both against the oracle: the
+    resources, multi-block frames and corruptions inside a 300-frame plan."""
+    import os
+    r = random.Random(79)
+    src = gen.text(300 * 4096, seed=15)
+    base = gen.frames(src, 4096, 3)
+    multi = gen.frames(gen.text(2 << 20, seed=16), 1 << 20, 9)
+    for mode in ("0", "1"):
+        os.environ["ZD_K3Q"] = mode
+        try:
+            for name, data in resources.items():
+                assert_parity(data, False, f"K3Q={mode} {name}")
+            assert_parity(multi, False, f"K3Q={mode} multi-block")
+            assert_parity(base, False, f"K3Q={mode} 300 frames")
+            for it in range(10):
+                d = bytearray(base)
+                for _ in range(r.randrange(1, 4)):
+                    d[r.randrange(len(d))] = r.randrange(256)
+                assert_parity(bytes(d), False, f"K3Q={mode} corrupt #{it}", allow_ood=True)
+        finally:
+            del os.environ["ZD_K3Q"]
+
+
 def test_plan_decompress_reuses_the_plan(resources):
     """zd_plan_decompress: host in / host out with a plan made once (the
     INTEGRATION.md decompress() pattern), equal to the oracle's output."""

@@ -1294,6 +1294,11 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // parity-green but slower than K4 on C4
   const char* k4p_env = getenv("ZD_K4P");
   a.k4_pipe = k4p_env && atoi(k4p_env) != 0;
+  // K3 as four lanes per block (K3Q, default): C3 (763 blocks) 2.89 -> 2.31
+  // ms, a forked 8,192-block plan 4.24 -> 2.48, full C4 13.88 -> 13.80;
+  // ZD_K3Q=0 (read per launch) keeps the one-lane chain
+  const char* k3q_env = getenv("ZD_K3Q");
+  a.k3_quad = !(k3q_env && atoi(k3q_env) == 0);
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
   // K2 beside K3 on a second stream: measured slower on C4 (61.4 vs 57.9 ms:

@@ -3689,16 +3689,16 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   auto k3 = [&](uint32_t l0, uint32_t l1) {
-    if (l1 > l0 && (a.kmask & 4))
-#ifdef ZD_K3_QUAD
-      hipLaunchKernelGGL(zd_k_sequences_q, dim3((l1 - l0 + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, s, a.src, comp,
-                         cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0, (const uint16_t*)fses,
-                         seqs);
-#else
-      hipLaunchKernelGGL(zd_k_sequences, dim3((l1 - l0 + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src, comp,
-                         cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0, (const uint16_t*)fses,
-                         seqs);
-#endif
+    if (l1 > l0 && (a.kmask & 4)) {
+      if (a.k3_quad)
+        hipLaunchKernelGGL(zd_k_sequences_q, dim3((l1 - l0 + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, s, a.src,
+                           comp, cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0,
+                           (const uint16_t*)fses, seqs);
+      else
+        hipLaunchKernelGGL(zd_k_sequences, dim3((l1 - l0 + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, s, a.src,
+                           comp, cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0,
+                           (const uint16_t*)fses, seqs);
+    }
   };
   auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st) {
     const uint32_t n = f1 - f0;

@@ -26,6 +26,7 @@ struct LaunchArgs {
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
   bool k4_pipe = false;    // streaming frames: the pipelined K4P (K4 for the context API's direct records)
+  bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block
   uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
 };
 
