@@ -223,9 +223,26 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* t
   }
   if (placed != zero_pos) return ZD_E_CORRUPTED_TABLE;
   for (uint32_t s = 0; s < nsym; s++) next[s] = dist[s] > 0 ? (uint16_t)dist[s] : (dist[s] == -1 ? 1 : 0);
-  for (uint32_t i = 0; i < T; i++) {
-    uint32_t s = sym[i];
-    table[i] = fse_entry(s, next[s]++);
+  // next[s]++ in state order, four states a step (T >= 32): one LDS round
+  // trip for the four counters instead of one per state; a symbol met again
+  // inside the step continues from its earlier value there, and the
+  // write-backs in state order leave each counter at its last value + 1
+  for (uint32_t i = 0; i < T; i += 4) {
+    const uint32_t w = *(const uint32_t*)(sym + i);
+    const uint32_t s0 = w & 255, s1 = (w >> 8) & 255, s2 = (w >> 16) & 255, s3 = w >> 24;
+    const uint32_t n0 = next[s0], n1 = next[s1], n2 = next[s2], n3 = next[s3];
+    const uint32_t t0 = n0;
+    const uint32_t t1 = s1 == s0 ? t0 + 1 : n1;
+    const uint32_t t2 = s2 == s1 ? t1 + 1 : (s2 == s0 ? t0 + 1 : n2);
+    const uint32_t t3 = s3 == s2 ? t2 + 1 : (s3 == s1 ? t1 + 1 : (s3 == s0 ? t0 + 1 : n3));
+    next[s0] = (uint16_t)(t0 + 1);
+    next[s1] = (uint16_t)(t1 + 1);
+    next[s2] = (uint16_t)(t2 + 1);
+    next[s3] = (uint16_t)(t3 + 1);
+    table[i] = fse_entry(s0, t0);
+    table[i + 1] = fse_entry(s1, t1);
+    table[i + 2] = fse_entry(s2, t2);
+    table[i + 3] = fse_entry(s3, t3);
   }
   return 0;
 }
