@@ -114,19 +114,25 @@ struct BwBits {
   }
 };
 
-// ForwardBitParser (parsing.rs:114-189), LSB-first, byte loads (headers only).
+// ForwardBitParser (parsing.rs:114-189), LSB-first (headers and table
+// descriptions).  A 64-bit cache of the bytes from the last refill: one 8-byte
+// load per ~40 bits read instead of two or three dependent byte loads per
+// peek (K1's NCount parse, C3: the sequence-table half 298 us).
 struct FwBits {
   const uint8_t* d;
   uint32_t nbytes;
   uint32_t pos;
-  __device__ inline uint32_t bits(uint32_t at, int len) const {   // len <= 24, within range
-    uint32_t v = 0;
-    uint32_t b0 = at >> 3, b1 = (at + len - 1) >> 3;
-    for (uint32_t b = b1 + 1; b-- > b0;) v = (v << 8) | d[b];
-    v >>= (at & 7);
+  uint64_t cache = 0;
+  int64_t cbit = -1;                               // bit of d that is cache bit 0 (-1: empty)
+  __device__ inline uint32_t bits(uint32_t at, int len) {   // len <= 24, within range
+    if (cbit < 0 || (int64_t)at < cbit || (int64_t)at + len > cbit + 64) {
+      cache = load_u64(d + (at >> 3), d, d + nbytes);
+      cbit = (int64_t)(at >> 3) * 8;
+    }
+    const uint32_t v = (uint32_t)(cache >> ((int64_t)at - cbit));
     return len >= 32 ? v : (v & ((1u << len) - 1));
   }
-  __device__ inline int peek(int len, uint32_t* v) const {
+  __device__ inline int peek(int len, uint32_t* v) {
     if ((int64_t)nbytes * 8 - pos < len) return ZD_E_NOT_ENOUGH_BITS;
     *v = len ? bits(pos, len) : 0;
     return 0;
