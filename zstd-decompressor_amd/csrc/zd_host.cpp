@@ -611,11 +611,29 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   return 0;
 }
 
-// K2 | K3 fork while K3 needs at most two workgroups per CU (256 CUs x 16
-// chains each): 8192 blocks 7.73 -> 7.40 ms per step, 16384 blocks 8.94 ->
-// 10.01 (scripts/exp_thresholds.sh)
-constexpr size_t FORK_MAX_SEQ_BLOCKS = 2 * 256 * 16;
+// K2 | K3 fork: it pays where K3's last round of chains leaves LDS for K2
+// beside it.  K3 holds 64 chains per CU (4 workgroups of 16); with the round's
+// fill f = (blocks mod 64 CUs) / (64 CUs), measured with K3Q on C4-shaped
+// plans (value, no fork -> fork): 10,240 blocks (f 0.63) 194 -> 221 GB/s,
+// 20,480 (0.25) 211 -> 234, 40,960 (0.5) 247 -> 253; 12,288 (0.75) 221 ->
+// 210, 16,384 (0) 251 -> 214, 32,768 (0) 266 -> 250, 81,920 (0) 273 -> 268;
+// 763 (C3) and 8,192 (0.5) fork.  So: fork when 0 < f <= 0.65.
 constexpr size_t FORK_MIN_SEQ_BLOCKS = 256;
+constexpr double FORK_MAX_FILL = 0.65;
+bool fork_auto(size_t n_seq) {
+  static int dev_cached = -1;
+  static size_t slots = 64 * 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev != dev_cached) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      slots = 64 * (size_t)cus;
+    dev_cached = dev;
+  }
+  if (n_seq < FORK_MIN_SEQ_BLOCKS) return false;
+  const size_t rem = n_seq % slots;
+  return rem != 0 && (double)rem <= FORK_MAX_FILL * (double)slots;
+}
 
 // Device workspaces of destroyed plans, kept for the next plans of this
 // process (a plan's workspace is up to ~1.2x its decoded bytes: K3's
@@ -1301,15 +1319,12 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.k3_quad = !(k3q_env && atoi(k3q_env) == 0);
   a.events = P->profile ? P->ev : nullptr;
   if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
-  // K2 beside K3 on a second stream: measured slower on C4 (61.4 vs 57.9 ms:
-  // K3 is LDS-bound and K2 takes its CUs), so it is taken only when K3's
-  // chains use at most two workgroups per CU (FORK_MAX_SEQ_BLOCKS: the few-
-  // frames regime, where both kernels run one round at their chain latency)
-  // and there are enough of them for the overlap to pay for a second stream;
-  // ZD_FORK=1 / 0 forces it on / off
+  // K2 beside K3 on a second stream: slower where K3's rounds fill the LDS
+  // (full C4: K3 is LDS-bound and K2 takes its CUs), faster where K3's last
+  // round leaves room (fork_auto); ZD_FORK=1 / 0 forces it on / off
   static const char* fork_env = getenv("ZD_FORK");
   const bool fork = fork_env ? atoi(fork_env) == 1
-                             : P->n_seq >= FORK_MIN_SEQ_BLOCKS && P->n_seq <= FORK_MAX_SEQ_BLOCKS;
+                             : fork_auto(P->n_seq);
   static const bool overlap = getenv("ZD_OVERLAP") && atoi(getenv("ZD_OVERLAP")) == 1;
   if (overlap && !fork && !P->staged && P->n_frames > 1) {
     // K4 of the first half of the frames beside K3 of the second half
