@@ -463,7 +463,9 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
+            # the one corpus split over the ranks (one rank: all of it), so the
+            # N = 1 line and the N > 1 lines are the same strong-scaling series
+            "scaling": "strong" if args.scaling == "strong" and args.workload != "c3s" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
