@@ -1044,6 +1044,18 @@ __device__ inline uint32_t winn_at(const WinN<N>& w, uint32_t y) {
   return __builtin_amdgcn_alignbit(hi, lo, y & 31);
 }
 
+// winn_at by the three bits of the dword index (N = 6): three selects deep
+// instead of five (few-chains regime: the step is the chain's latency)
+template <int N>
+__device__ inline uint32_t winn_at_tree(const WinN<N>& w, uint32_t y) {
+  static_assert(N == 6, "tree select for 6-dword windows");
+  const bool b0 = (y & 32) != 0, b1 = (y & 64) != 0, b2 = y >= 128;
+  const uint32_t l01 = b0 ? w.w[1] : w.w[0], l23 = b0 ? w.w[3] : w.w[2], l45 = b0 ? w.w[5] : w.w[4];
+  const uint32_t h01 = b0 ? w.w[2] : w.w[1], h23 = b0 ? w.w[4] : w.w[3], h45 = b0 ? 0u : w.w[5];
+  const uint32_t lo = b2 ? l45 : (b1 ? l23 : l01), hi = b2 ? h45 : (b1 ? h23 : h01);
+  return __builtin_amdgcn_alignbit(hi, lo, y & 31);
+}
+
 // The fast chain: no checks inside the loop.  Each table gives nextState and
 // the step's total bit count for that table (k3f_entry), so a step is
 // pos -= tLL + tML + tOF, then the LL | ML | OF state bits are the low bits
@@ -1308,17 +1320,37 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   }
   uint32_t mx = 0;
   int32_t ymin = 0;
+#ifdef ZD_K3Q_ADDR
+  const lds_u16* tp = tab + s;
+#endif
   auto step = [&](WinN<N>& use) -> uint64_t {
+#ifdef ZD_K3Q_ADDR
+    const uint32_t e = *tp;
+#else
     const uint32_t e = tab[s];
+#endif
     mx = max(mx, e & m3);
     const uint32_t ns = e & 1023, nb = __builtin_clz(ns) + ar;
-    pos -= (int32_t)quad_sum((e >> 10) & m3);
-    const int32_t y = pos - use.wb;
+    // the three roles' counts by three quad broadcasts and one add3 (the
+    // shadow lane's count never enters), y from the position before the step
+    // (C3 K3 2.31 -> 2.22 ms)
+    const uint32_t c = e >> 10;
+    const uint32_t csum = qdpp<0x00>(c) + qdpp<0x55>(c) + qdpp<0xAA>(c);
+    const int32_t y = (pos - use.wb) - (int32_t)csum;
+    pos -= (int32_t)csum;
     ymin = min(ymin, y);
-    const uint32_t r = winn_at<N>(use, (uint32_t)y);
+    const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
     use = winn_load<N>(bs, m, pos);
     const uint32_t v = __builtin_amdgcn_ubfe(r, quad_excl(nb, m0), nb);
+#ifdef ZD_K3Q_ADDR
+    // the next entry's address from v in one op: base + 2 ((ns << nb) - T)
+    // is formed beside the window select
+    const uint32_t nsT = (ns << nb) - Tr;
+    tp = tab + nsT + v;
+    s = nsT + v;
+#else
     s = (ns << nb) + v - Tr;
+#endif
     return (uint64_t)(uint32_t)pos | ((uint64_t)quad_or((s << shr) & m3) << 32);
   };
   for (uint32_t i = 0; i + 1 < n; i += U) {
