@@ -1048,11 +1048,21 @@ __device__ inline uint32_t winn_at(const WinN<N>& w, uint32_t y) {
 // instead of five (few-chains regime: the step is the chain's latency)
 template <int N>
 __device__ inline uint32_t winn_at_tree(const WinN<N>& w, uint32_t y) {
-  static_assert(N == 6, "tree select for 6-dword windows");
+  static_assert(N == 6 || N == 8, "tree select for 6- or 8-dword windows");
   const bool b0 = (y & 32) != 0, b1 = (y & 64) != 0, b2 = y >= 128;
   const uint32_t l01 = b0 ? w.w[1] : w.w[0], l23 = b0 ? w.w[3] : w.w[2], l45 = b0 ? w.w[5] : w.w[4];
-  const uint32_t h01 = b0 ? w.w[2] : w.w[1], h23 = b0 ? w.w[4] : w.w[3], h45 = b0 ? 0u : w.w[5];
-  const uint32_t lo = b2 ? l45 : (b1 ? l23 : l01), hi = b2 ? h45 : (b1 ? h23 : h01);
+  const uint32_t h01 = b0 ? w.w[2] : w.w[1], h23 = b0 ? w.w[4] : w.w[3];
+  uint32_t lo, hi;
+  if constexpr (N == 6) {
+    const uint32_t h45 = b0 ? 0u : w.w[5];
+    lo = b2 ? l45 : (b1 ? l23 : l01);
+    hi = b2 ? h45 : (b1 ? h23 : h01);
+  } else {
+    const uint32_t l67 = b0 ? w.w[7] : w.w[6];
+    const uint32_t h45 = b0 ? w.w[6] : w.w[5], h67 = b0 ? 0u : w.w[7];
+    lo = b2 ? (b1 ? l67 : l45) : (b1 ? l23 : l01);
+    hi = b2 ? (b1 ? h67 : h45) : (b1 ? h23 : h01);
+  }
   return __builtin_amdgcn_alignbit(hi, lo, y & 31);
 }
 
@@ -1320,15 +1330,8 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   }
   uint32_t mx = 0;
   int32_t ymin = 0;
-#ifdef ZD_K3Q_ADDR
-  const lds_u16* tp = tab + s;
-#endif
   auto step = [&](WinN<N>& use) -> uint64_t {
-#ifdef ZD_K3Q_ADDR
-    const uint32_t e = *tp;
-#else
     const uint32_t e = tab[s];
-#endif
     mx = max(mx, e & m3);
     const uint32_t ns = e & 1023, nb = __builtin_clz(ns) + ar;
     // the three roles' counts by three quad broadcasts and one add3 (the
@@ -1342,15 +1345,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
     use = winn_load<N>(bs, m, pos);
     const uint32_t v = __builtin_amdgcn_ubfe(r, quad_excl(nb, m0), nb);
-#ifdef ZD_K3Q_ADDR
-    // the next entry's address from v in one op: base + 2 ((ns << nb) - T)
-    // is formed beside the window select
-    const uint32_t nsT = (ns << nb) - Tr;
-    tp = tab + nsT + v;
-    s = nsT + v;
-#else
-    s = (ns << nb) + v - Tr;
-#endif
+    s = (ns << nb) + v - Tr;   // (the next address formed from v in one op: 2.07 -> 2.11 ms on C3)
     return (uint64_t)(uint32_t)pos | ((uint64_t)quad_or((s << shr) & m3) << 32);
   };
   for (uint32_t i = 0; i + 1 < n; i += U) {
