@@ -635,12 +635,15 @@ __device__ inline uint32_t win6_bits(const Win6& w, int32_t p, uint32_t S) {
 __device__ inline uint64_t win6_top64(const Win6& w, int32_t q) {
   const uint32_t y = (uint32_t)(q - 32 - w.wb);          // bit offset of the top dword's low end
   const uint32_t k = y >> 5, sh = y & 31;                // k in [0, 5]
-  uint32_t a = 0u, b = w.w0, c = w.w1;                   // w[k-1], w[k], w[k+1]
-  a = k >= 1 ? w.w0 : a; b = k >= 1 ? w.w1 : b; c = k >= 1 ? w.w2 : c;
-  a = k >= 2 ? w.w1 : a; b = k >= 2 ? w.w2 : b; c = k >= 2 ? w.w3 : c;
-  a = k >= 3 ? w.w2 : a; b = k >= 3 ? w.w3 : b; c = k >= 3 ? w.w4 : c;
-  a = k >= 4 ? w.w3 : a; b = k >= 4 ? w.w4 : b; c = k >= 4 ? w.w5 : c;
-  a = k >= 5 ? w.w4 : a; b = k >= 5 ? w.w5 : b; c = k >= 5 ? 0u : c;
+  // w[k-1], w[k], w[k+1] by the three bits of k: three selects deep
+  // (a 5-deep chain of k >= i selects: K2 on C4 4 GiB 2.21 ms, this 2.18-2.20)
+  const bool b0 = (k & 1) != 0, b1 = (k & 2) != 0, b2 = k >= 4;
+  const uint32_t a01 = b0 ? w.w0 : 0u, a23 = b0 ? w.w2 : w.w1, a45 = b0 ? w.w4 : w.w3;
+  const uint32_t b01 = b0 ? w.w1 : w.w0, b23 = b0 ? w.w3 : w.w2, b45 = b0 ? w.w5 : w.w4;
+  const uint32_t c01 = b0 ? w.w2 : w.w1, c23 = b0 ? w.w4 : w.w3, c45 = b0 ? 0u : w.w5;
+  const uint32_t a = b2 ? a45 : (b1 ? a23 : a01);
+  const uint32_t b = b2 ? b45 : (b1 ? b23 : b01);
+  const uint32_t c = b2 ? c45 : (b1 ? c23 : c01);
   const uint32_t hi = __builtin_amdgcn_alignbit(c, b, sh), lo = __builtin_amdgcn_alignbit(b, a, sh);
   return ((uint64_t)hi << 32) | lo;
 }
