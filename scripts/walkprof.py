@@ -1,6 +1,13 @@
-import os, sys, time
-sys.path[:0] = ["/root/repo", "/root/repo/zstd-decompressor_amd"]
-os.environ.setdefault("ZD_LIB_PATH", "zstd-decompressor_amd/lib/variants/libzd_walkprof.so")
+"""Device header walk vs host walk plan times on a 1 GiB C4-shaped input.
+Per-range scan / walk cycles: build `make -C zstd-decompressor_amd variant
+NAME=walkprof DEFS=-DZD_WALK_PROF` and run with
+ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_walkprof.so (and
+ZD_PLAN_TIMES=1 for the planner phases)."""
+import os
+import sys
+import time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "zstd-decompressor_amd")]
 import torch
 from corpus import gen
 from zstd_decompressor.batch import Plan
