@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 4
+#define ZD_ABI_VERSION 5
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -76,8 +76,9 @@ extern "C" {
 #define ZD_E_COMM            (-97) /* an RCCL call failed, or RCCL is not loadable */
 
 /* Device workspaces of destroyed plans are kept for reuse by later plans of
- * the process (bounded by ZD_WS_CACHE_MB, default 32 GiB; 0 disables it).
- * zd_trim_cache frees them (every device). */
+ * the process (bounded by ZD_WS_CACHE_MB, default 8 GiB; 0 disables it).
+ * zd_trim_cache frees them (every device): PyTorch's caching allocator does
+ * not see this memory. */
 void zd_trim_cache(void);
 
 /* Human-readable name of a status code (static storage). */
@@ -147,6 +148,9 @@ typedef struct zd_plan zd_plan;
  * automatic.  Same output either way; tests run both. */
 #define ZD_F_BLOCK_PARALLEL 2u  /* every frame with a compressed block -> K4J (block-parallel execute) */
 #define ZD_F_FRAME_SERIAL   4u  /* no frame -> K4J (the streaming per-frame executor) */
+/* Sequence-decode choice: K3 with one lane per block instead of four (the
+ * default, K3Q).  Same records either way; tests run both. */
+#define ZD_F_SEQ_ONE_LANE   8u
 
 typedef struct zd_plan_info {
   uint64_t nframes;        /* frames in the plan (skippable included) */
@@ -162,6 +166,11 @@ typedef struct zd_plan_info {
   uint32_t _pad;
   uint64_t host_ns;        /* zd_plan_create: header walk + descriptors (host work) */
   uint64_t device_ns;      /* zd_plan_create: workspace allocation + descriptor upload */
+  uint64_t walk_serial_bytes; /* input bytes the frame walk had to walk serially (a range whose
+                                 parallel walk started at a magic number inside data); 0 normally */
+  uint64_t io_h2d_ns;      /* the last zd_plan_decompress: input host -> HBM */
+  uint64_t io_decode_ns;   /*   decode + results (kernels, status read-back) */
+  uint64_t io_d2h_ns;      /*   output HBM -> host */
 } zd_plan_info;
 
 /* Index src[0..n) on the host and allocate the plan's device workspace.
@@ -224,7 +233,11 @@ int zd_plan_set_profiling(zd_plan* plan, int enable);
 int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, int* n);
 
 /* zd_decompress with a plan already made for the same n bytes (so a caller
- * that sized dst from zd_plan_info_get does not plan twice). */
+ * that sized dst from zd_plan_info_get does not plan twice).  The plan keeps
+ * the device buffers for the next call (freed by zd_plan_destroy); input and
+ * output move through pinned chunks (zd_plan_info io_*_ns: the phases of the
+ * last call).  Not thread-safe against other zd_plan_decompress calls of the
+ * process (they serialise on the pinned ring). */
 int zd_plan_decompress(zd_plan* plan, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 /* Convenience: host in, host out (H2D + decode + D2H on the default
  * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
@@ -269,6 +282,17 @@ typedef struct zd_gather_result {
   int32_t failed_rank;        /* that rank, or world when none failed */
   int64_t first_error_frame;  /* global index of the first failing frame, -1 if none */
 } zd_gather_result;
+
+/* Host only: the outcome merge every rank of zd_comm_gather performs on the
+ * all-gathered outcomes.  meta = world x 4 int64 {status, first failing frame
+ * (global, -1 if none), local length, root capacity (rank 0's entry; 0
+ * elsewhere)}.  The output stops at the first failing rank's failure: that
+ * rank keeps its frames before the failure (its local length), later ranks
+ * contribute nothing (src/main.rs:43-53).  Fills off[r] / len[r] (world
+ * entries: where rank r's bytes land on rank 0, and how many) and *res;
+ * returns ZD_E_DST_TOO_SMALL (res->total_len 0: nothing may be sent) when the
+ * kept bytes exceed rank 0's capacity. */
+int zd_gather_layout(const int64_t* meta, int world, uint64_t* off, uint64_t* len, zd_gather_result* res);
 
 /* Collective (every rank calls it): each rank's outcome — status, first
  * failing frame (global index), decoded length — is all-gathered; the output

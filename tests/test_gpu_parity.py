@@ -18,16 +18,16 @@ pytestmark = pytest.mark.gpu
 REF_PANIC, OUT_OF_DOMAIN = -90, -91
 
 
-def gpu(data, p=False):
+def gpu(data, p=False, flags=0):
     from zstd_decompressor.batch import decompress_status
-    return decompress_status(data, p)
+    return decompress_status(data, p, flags)
 
 
-def assert_parity(data, p=False, what="", allow_ood=False):
+def assert_parity(data, p=False, what="", allow_ood=False, flags=0):
     """allow_ood: the input may leave the GPU path's domain (corrupted input
     decoding past its declared content size)."""
     ost, oout = oracle.decompress_status(data, p)
-    gst, gout = gpu(data, p)
+    gst, gout = gpu(data, p, flags)
     if allow_ood and gst == OUT_OF_DOMAIN:
         return ost, gst
     if ost == 0:
@@ -257,28 +257,25 @@ def test_many_frame_roundtrip_large():
 
 
 def test_one_lane_k3_chain(resources):
-    """K3 runs four lanes per block by default (K3Q, seq_chainq); ZD_K3Q=0
-    keeps the one-lane chain (seq_chainfl).  Both against the oracle: the
-    resources, multi-block frames and corruptions inside a 300-frame plan."""
-    import os
+    """K3 runs four lanes per block by default (K3Q, seq_chainq); the plan flag
+    ZD_F_SEQ_ONE_LANE keeps the one-lane chain (seq_chainfl).  Both against
+    the oracle: the resources, multi-block frames and corruptions inside a
+    300-frame plan."""
+    from zstd_decompressor import _lib
     r = random.Random(79)
     src = gen.text(300 * 4096, seed=15)
     base = gen.frames(src, 4096, 3)
     multi = gen.frames(gen.text(2 << 20, seed=16), 1 << 20, 9)
-    for mode in ("0", "1"):
-        os.environ["ZD_K3Q"] = mode
-        try:
-            for name, data in resources.items():
-                assert_parity(data, False, f"K3Q={mode} {name}")
-            assert_parity(multi, False, f"K3Q={mode} multi-block")
-            assert_parity(base, False, f"K3Q={mode} 300 frames")
-            for it in range(10):
-                d = bytearray(base)
-                for _ in range(r.randrange(1, 4)):
-                    d[r.randrange(len(d))] = r.randrange(256)
-                assert_parity(bytes(d), False, f"K3Q={mode} corrupt #{it}", allow_ood=True)
-        finally:
-            del os.environ["ZD_K3Q"]
+    for flags in (_lib.F_SEQ_ONE_LANE, 0):
+        for name, data in resources.items():
+            assert_parity(data, False, f"flags={flags} {name}", flags=flags)
+        assert_parity(multi, False, f"flags={flags} multi-block", flags=flags)
+        assert_parity(base, False, f"flags={flags} 300 frames", flags=flags)
+        for it in range(10):
+            d = bytearray(base)
+            for _ in range(r.randrange(1, 4)):
+                d[r.randrange(len(d))] = r.randrange(256)
+            assert_parity(bytes(d), False, f"flags={flags} corrupt #{it}", allow_ood=True, flags=flags)
 
 
 def test_plan_decompress_reuses_the_plan(resources):

@@ -68,3 +68,25 @@ def test_device_walk_plan_equals_host_walk(resources, tmp_path):
                 assert _decode(dp, d_src, dev) == _decode(hp, d_src, dev), name
             hp.close()
             dp.close()
+
+
+def test_device_walk_false_frame_costs_one_range():
+    """A planted magic number that parses as a whole frame, first in device
+    range 4 (256 KiB ranges): the stitch walks on the device one range at a
+    time until the chain meets a later range's (it used to walk the rest of
+    the input as one serial range); the plan still equals the host walk's."""
+    import torch
+    import test_host_walk
+    from zstd_decompressor.batch import Plan
+    dev = torch.device("cuda", 0)
+    data, rsize, at = test_host_walk.false_frame_input(cut=4 << 18)
+    d_src = torch.zeros(len(data) + 64, dtype=torch.uint8, device=dev)
+    d_src[: len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    torch.cuda.synchronize(dev)
+    hp = Plan(data)
+    dp = Plan.from_device(d_src.data_ptr(), len(data), stream=torch.cuda.current_stream(dev).cuda_stream)
+    assert 0 < dp.info.walk_serial_bytes <= 2 * (256 << 10), dp.info.walk_serial_bytes
+    assert dp.info.nframes == hp.info.nframes and dp.info.index_status == hp.info.index_status == 0
+    assert _decode(dp, d_src, dev) == _decode(hp, d_src, dev)
+    hp.close()
+    dp.close()

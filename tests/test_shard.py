@@ -237,3 +237,118 @@ def test_comm_gather_and_sharded_decode_world1_gpu():
     p.join(timeout=60)
     assert p.exitcode == 0
     assert got == (True, True)
+
+
+def _layout_py(meta, world):
+    """shard.collect's rule on all-gathered outcomes: (status, first frame,
+    failing rank, kept lengths)."""
+    failed = next((r for r in range(world) if meta[r][0] != 0), world)
+    lens = [meta[r][2] if r <= failed else 0 for r in range(world)]
+    st = meta[failed][0] if failed < world else 0
+    first = meta[failed][1] if failed < world else -1
+    return st, first, failed, lens
+
+
+def _layout_c(meta, world):
+    import ctypes as C
+    from zstd_decompressor import _lib
+    flat = (C.c_int64 * (4 * world))(*[v for row in meta for v in row])
+    off = (C.c_uint64 * world)()
+    ln = (C.c_uint64 * world)()
+    res = _lib.GatherResult()
+    st = _lib.lib().zd_gather_layout(flat, world, off, ln, C.byref(res))
+    return st, res, list(off), list(ln)
+
+
+def test_gather_layout_host_only():
+    """zd_gather_layout (the merge every rank of zd_comm_gather runs on the
+    all-gathered outcomes; host only, so it runs here) against shard.collect's
+    rule at world 1/2/3/8: clean, a failing middle rank, a failing rank 0 and
+    last rank, empty ranks, and rank 0's capacity limit."""
+    import random
+    from zstd_decompressor import _lib
+    r = random.Random(8)
+    for world in (1, 2, 3, 8):
+        for trial in range(200):
+            lens = [r.choice([0, 1, 17, 4096, 1 << 20]) for _ in range(world)]
+            sts = [0] * world
+            fail = r.choice([None] + list(range(world)))
+            if fail is not None:
+                sts[fail] = r.choice([_lib.IMPOSSIBLE_VALUE, _lib.NOT_ENOUGH_BYTES, _lib.OUT_OF_DOMAIN])
+                if r.random() < 0.5 and fail + 1 < world:
+                    sts[r.randrange(fail + 1, world)] = _lib.NULL_OFFSET     # a later failure does not count
+            firsts = [r.randrange(0, 1000) if s else -1 for s in sts]
+            need = sum(lens[: (fail if fail is not None else world - 1) + 1])
+            cap = r.choice([need, need + 5, max(need - 1, 0), 1 << 40])
+            meta = [[sts[k], firsts[k], lens[k], cap if k == 0 else 0] for k in range(world)]
+            st, first, failed, klens = _layout_py(meta, world)
+            cst, res, off, ln = _layout_c(meta, world)
+            assert (res.status, res.first_error_frame, res.failed_rank) == (st, first, failed)
+            if sum(klens) > cap:
+                assert cst == _lib.DST_TOO_SMALL and res.total_len == 0
+            else:
+                assert cst == 0 and res.total_len == sum(klens)
+                assert ln == klens and off == [sum(klens[:k]) for k in range(world)]
+
+
+def _worker_layout(rank, world, port, payloads, statuses, cap, q):
+    """Every rank: shard.collect over gloo (the Python gather) and the C-ABI
+    merge on the same all-gathered outcomes; both must agree on every rank."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = payloads[rank]
+        st, first = statuses[rank]
+        meta = torch.tensor([st, first if st else -1, len(mine), cap if rank == 0 else 0], dtype=torch.int64)
+        alls = [torch.zeros(4, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(alls, meta)
+        cst, res, off, ln = _layout_c([t.tolist() for t in alls], world)
+        local = torch.frombuffer(bytearray(mine + b"\x55" * 3), dtype=torch.uint8)
+        gst, gfirst, n, out = shard.collect(local, len(mine), st, first, rank, world)
+        q.put((rank, cst, res.status, res.first_error_frame, res.total_len, off, ln, gst, gfirst, n,
+               None if out is None else bytes(out.numpy().tobytes())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail,short", [(2, None, False), (3, 1, False), (8, 5, False), (8, None, True)])
+def test_gather_layout_multi_rank_gloo(world, fail, short):
+    """zd_comm_gather's merge at world 2/3/8 on CPU ranks (gloo), beside
+    shard.collect: the same status / first failing frame on every rank, each
+    rank's kept length, rank 0's offsets tile the gathered bytes, and a short
+    root capacity refuses on every rank (nothing would be sent)."""
+    from zstd_decompressor import _lib
+    payloads = [bytes([65 + r]) * (100 + 37 * r) for r in range(world)]
+    statuses = [(0, -1)] * world
+    if fail is not None:
+        statuses[fail] = (_lib.IMPOSSIBLE_VALUE, 1000 + fail)
+    upto = (fail if fail is not None else world - 1) + 1
+    need = sum(len(p) for p in payloads[:upto])
+    cap = need - 1 if short else need
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_layout, args=(r, world, port, payloads, statuses, cap, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        v = q.get(timeout=180)
+        got[v[0]] = v[1:]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        cst, rst, rfirst, total, off, ln, gst, gfirst, n, out = got[r]
+        assert (rst, rfirst) == (gst, gfirst)
+        assert ln[r] == n                                   # the kept length matches collect's cut
+        if short:
+            assert cst == _lib.DST_TOO_SMALL and total == 0
+        else:
+            assert cst == 0 and total == need
+    if not short:
+        out = got[0][-1]
+        _, _, _, _, off, ln, *_ = got[0]
+        assert out == b"".join(payloads[:upto])
+        assert all(out[off[k]: off[k] + ln[k]] == payloads[k][: ln[k]] for k in range(world))

@@ -23,6 +23,7 @@
 
 #include "../../include/zd.h"
 #include "zd_common.h"
+#include "zd_internal.h"
 #include "zd_launch.h"
 #include "zd_walk.h"
 
@@ -79,6 +80,7 @@ struct zd_plan {
   Workspace W{};
   uint8_t* d_ws = nullptr;
   uint64_t ws_bytes = 0;                 // size of the d_ws allocation (>= W.total: a cached block)
+  int dev = -1;                          // the device d_ws and the aux stream belong to (upload_plan)
   uint64_t desc_bytes = 0;               // the host-filled head of the workspace (one upload)
   uint8_t* d_staging = nullptr;          // when the output layout is not exact
   uint64_t staging_bytes = 0;
@@ -106,6 +108,13 @@ struct zd_plan {
   hipEvent_t fork = nullptr, join = nullptr;
   // output layout of the last zd_plan_results (frames before the first failure)
   std::vector<uint64_t> res_off, res_len;
+  uint64_t* d_meta = nullptr;            // zd_plan_results' compaction / zd_plan_checksums' arrays
+  uint64_t meta_cap = 0;                 // (u64 entries)
+  // zd_plan_decompress (host in, host out): device buffers kept between calls
+  uint8_t* io_src = nullptr;
+  uint64_t io_src_cap = 0;
+  uint8_t* io_dst = nullptr;
+  uint64_t io_dst_cap = 0;
 };
 
 namespace {
@@ -126,6 +135,7 @@ constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 3 * 256;
 constexpr uint32_t K4J_MIN_BLOCKS = 16;
 constexpr size_t K4J_MAX_FRAMES = 1024;
 constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
+constexpr size_t FRAMES_INDEX_SERIAL_MAX = 4096;     // zd_frames_index asked for at most this many frames: walk only them
 
 // Running indices of build_plan: every array it fills grows frame by frame,
 // so a frame's entries start at the counts of the frames before it.
@@ -640,7 +650,9 @@ bool fork_auto(size_t n_seq) {
 // records, the literals, the tables).  A plan takes a cached block of at
 // least its size and at most 1.25x + 64 MiB; zd_trim_cache() frees them all,
 // and so does a failed allocation before its retry.  ZD_WS_CACHE_MB caps
-// the bytes held (default 32 GiB; 0 disables the cache).
+// the bytes held (default 8 GiB, at most 4 blocks; 0 disables the cache).
+// The cache is invisible to PyTorch's allocator: a torch user that needs the
+// memory back calls zd_trim_cache.
 struct WsCache {
   struct E { int dev; uint8_t* p; uint64_t bytes; };
   std::mutex m;
@@ -653,7 +665,7 @@ WsCache& ws_cache() {
 }
 uint64_t ws_cache_limit() {
   static const uint64_t lim = getenv("ZD_WS_CACHE_MB") ? strtoull(getenv("ZD_WS_CACHE_MB"), nullptr, 0) << 20
-                                                       : 32ull << 30;
+                                                       : 8ull << 30;
   return lim;
 }
 void ws_trim(int dev) {           // dev < 0: every device
@@ -669,9 +681,7 @@ void ws_trim(int dev) {           // dev < 0: every device
     }
   }
 }
-hipError_t ws_alloc(uint64_t bytes, uint8_t** p, uint64_t* got) {
-  int dev = 0;
-  if (hipError_t e = hipGetDevice(&dev)) return e;
+hipError_t ws_alloc(int dev, uint64_t bytes, uint8_t** p, uint64_t* got) {
   {
     WsCache& C = ws_cache();
     std::lock_guard<std::mutex> g(C.m);
@@ -699,11 +709,11 @@ hipError_t ws_alloc(uint64_t bytes, uint8_t** p, uint64_t* got) {
   *got = bytes;
   return e;
 }
-void ws_release(uint8_t* p, uint64_t bytes) {
+// (dev: the device p was allocated on, whatever device is current now)
+void ws_release(uint8_t* p, uint64_t bytes, int dev) {
   if (!p) return;
-  int dev = 0;
   const uint64_t lim = ws_cache_limit();
-  if (hipGetDevice(&dev) != hipSuccess || bytes > lim) { (void)hipFree(p); return; }
+  if (dev < 0 || bytes > lim) { (void)hipFree(p); return; }
   WsCache& C = ws_cache();
   std::lock_guard<std::mutex> g(C.m);
   C.free.push_back(WsCache::E{dev, p, bytes});
@@ -716,7 +726,8 @@ void ws_release(uint8_t* p, uint64_t bytes) {
 }
 
 int upload_plan(zd_plan* P) {
-  HIPCHK(ws_alloc(P->W.total, &P->d_ws, &P->ws_bytes));
+  HIPCHK(hipGetDevice(&P->dev));
+  HIPCHK(ws_alloc(P->dev, P->W.total, &P->d_ws, &P->ws_bytes));
   if (P->staged) {
     // the descriptors are in the pinned staging at their workspace offsets
     const hipError_t e = hipMemcpy(P->d_ws, host_stage().p, P->desc_bytes, hipMemcpyHostToDevice);
@@ -761,8 +772,8 @@ std::vector<AuxSet>& aux_free() {
   return *v;
 }
 bool aux_take(zd_plan* P) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const int dev = P->dev;                 // upload_plan's device (current here)
+  if (dev < 0) return false;
   {
     std::lock_guard<std::mutex> g(aux_mutex());
     auto& v = aux_free();
@@ -778,8 +789,8 @@ bool aux_take(zd_plan* P) {
          hipEventCreateWithFlags(&P->join, hipEventDisableTiming) == hipSuccess;
 }
 void aux_give(zd_plan* P) {
-  int dev = 0;
-  if (P->aux && P->fork && P->join && hipGetDevice(&dev) == hipSuccess) {
+  const int dev = P->dev;                 // the plan's device, not the current one
+  if (P->aux && P->fork && P->join && dev >= 0) {
     std::lock_guard<std::mutex> g(aux_mutex());
     if (aux_free().size() < 8) {
       aux_free().push_back(AuxSet{dev, P->aux, P->fork, P->join});
@@ -805,6 +816,18 @@ int index_frames(const uint8_t* src, Bytes& in, size_t stop, HostPart& part) {
     if (r) return r;
   }
   return 0;
+}
+
+// Index of the frame of a chain (frames in input order) that starts at byte
+// `at`, or SIZE_MAX.
+template <typename FR>
+size_t chain_start(const FR& frames, size_t at, size_t count = SIZE_MAX) {
+  size_t lo = 0, hi = std::min(count, (size_t)frames.size());
+  while (lo < hi) {
+    const size_t m = lo + (hi - lo) / 2;
+    if (frames[m].d.src_offset < at) lo = m + 1; else hi = m;
+  }
+  return (lo < std::min(count, (size_t)frames.size()) && frames[lo].d.src_offset == at) ? lo : SIZE_MAX;
 }
 
 inline bool magic_at(const uint8_t* p) {
@@ -863,35 +886,56 @@ int plan_index(zd_plan* P, const uint8_t* src, size_t n) {
   std::vector<HostPart> keep;
   int status = 0;
   size_t cur = 0;                                // where the kept frames end
-  for (size_t k = 0; k < T && !status; k++) {
-    if (k && cur >= cut[k + 1]) continue;        // the range lies inside a kept frame
-    HostPart& hp = part[k];
-    size_t i = 0;
-    while (i < hp.frames.size() && hp.frames[i].d.src_offset < cur) i++;
-    if (k && (i == hp.frames.size() || hp.frames[i].d.src_offset != cur)) {
-      // the chains do not meet: the rest of the input serially
-      HostPart tail;
-      Bytes in{src + cur, n - cur};
-      status = index_frames(src, in, SIZE_MAX, tail);
-      keep.push_back(std::move(tail));
-      cur = n;
-      break;
+  uint64_t serial = 0;                           // bytes the stitch walked itself
+  for (size_t k = 0; k < T && !status;) {
+    if (k && cur >= cut[k + 1]) { k++; continue; }   // the range lies inside a kept frame
+    const size_t i = k ? chain_start(part[k].frames, cur) : 0;
+    if (i != SIZE_MAX) {
+      HostPart& hp = part[k];
+      if (i) hp.frames.erase(hp.frames.begin(), hp.frames.begin() + (long)i);   // their blocks stay unreferenced
+      status = st[k];
+      cur = end[k];
+      keep.push_back(std::move(hp));
+      k++;
+      continue;
     }
-    if (i) hp.frames.erase(hp.frames.begin(), hp.frames.begin() + (long)i);   // their blocks stay unreferenced
-    status = st[k];
-    cur = end[k];
-    keep.push_back(std::move(hp));
+    // The chains do not meet (range k's walk started at a magic number
+    // inside data, or its first frame starts in an earlier range): walk on
+    // from cur frame by frame, only until a frame ends where a later range's
+    // chain has a frame start, then stitch on from that range.  One planted
+    // magic number costs at most the ranges it spoils, never the rest of the
+    // input (the walks from a given position are identical).
+    HostPart tail;
+    Bytes in{src + cur, n - cur};
+    size_t kk = k;
+    while (in.n) {
+      HostFrame hf;
+      VecSink sink{tail.blocks};
+      const int r = index_frame(src, in, &hf, sink);
+      tail.frames.push_back(hf);
+      const size_t p = (size_t)(in.p - src);
+      serial += p - cur;
+      cur = p;
+      if (r) { status = r; break; }
+      while (kk + 1 < T && cur >= cut[kk + 1]) kk++;
+      if (kk > k && chain_start(part[kk].frames, cur) != SIZE_MAX) break;
+    }
+    keep.push_back(std::move(tail));
+    k = kk > k ? kk : T;
   }
   const auto tw1 = std::chrono::steady_clock::now();
   P->set_parts(std::move(keep));
   if (getenv("ZD_PLAN_TIMES")) {
     fprintf(stderr, "zd walk: %zu threads, threads", T);
     for (double t : tms) fprintf(stderr, " %.1f", t);
-    fprintf(stderr, " ms; walk %.2f ms, stitch %.2f ms\n", std::chrono::duration<double, std::milli>(tw1 - tw0).count(),
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count());
+    fprintf(stderr, " ms; walk %.2f ms, stitch %.2f ms, serial %llu bytes\n",
+            std::chrono::duration<double, std::milli>(tw1 - tw0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count(),
+            (unsigned long long)serial);
   }
   P->index_status = status;
   P->index_stop = P->nframes;
+  P->info.walk_serial_bytes = serial;
   return 0;
 }
 
@@ -941,6 +985,79 @@ bool grow_pinned(T*& p, size_t& cap, size_t need) {
   if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) return false;
   cap = n;
   return true;
+}
+
+// zd_plan_decompress's host <-> device path: a process-wide ring of two
+// pinned chunks.  H2D: chunk k is copied into its pinned slot by the worker
+// pool while chunk k - 1's DMA runs; D2H: chunk k + 1's DMA runs while chunk
+// k is copied out.  (A pageable hipMemcpy stages through the runtime's own
+// buffers with one thread.)  Without pinned memory it falls back to that.
+constexpr uint64_t IO_CHUNK = 32ull << 20;
+struct IoRing {
+  std::mutex m;
+  uint8_t* p[2] = {nullptr, nullptr};
+  bool tried = false;
+  bool ok() {
+    if (!tried) {
+      tried = true;
+      for (auto& b : p)
+        if (hipHostMalloc((void**)&b, IO_CHUNK, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); b = nullptr; }
+      if (!p[0] || !p[1]) {
+        for (auto& b : p) if (b) (void)hipHostFree(b);
+        p[0] = p[1] = nullptr;
+      }
+    }
+    return p[0] != nullptr;
+  }
+};
+IoRing& io_ring() {
+  static IoRing* r = new IoRing();   // never destroyed (no HIP calls at exit)
+  return *r;
+}
+struct IoEvents {
+  hipEvent_t e[2] = {nullptr, nullptr};
+  bool ok = true;
+  IoEvents() {
+    for (auto& x : e) ok = ok && hipEventCreateWithFlags(&x, hipEventDisableTiming) == hipSuccess;
+  }
+  ~IoEvents() { for (auto& x : e) if (x) (void)hipEventDestroy(x); }
+};
+void par_memcpy(uint8_t* d, const uint8_t* s, size_t n) {
+  const size_t T = std::min<size_t>(16, std::max<size_t>(1, n >> 21));   // >= 2 MiB a thread
+  run_parts(T, [&](size_t k) {
+    const size_t a = n * k / T, b = n * (k + 1) / T;
+    memcpy(d + a, s + a, b - a);
+  });
+}
+int io_h2d(uint8_t* d, const uint8_t* h, size_t n, hipStream_t s, IoRing& R, hipEvent_t ev[2]) {
+  if (!n) return 0;
+  if (!R.ok()) { HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s)); return 0; }
+  for (size_t o = 0, k = 0; o < n; o += IO_CHUNK, k++) {
+    const size_t c = std::min<size_t>(IO_CHUNK, n - o);
+    if (k >= 2) HIPCHK(hipEventSynchronize(ev[k & 1]));   // chunk k - 2's DMA out of this slot
+    par_memcpy(R.p[k & 1], h + o, c);
+    HIPCHK(hipMemcpyAsync(d + o, R.p[k & 1], c, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(ev[k & 1], s));
+  }
+  return 0;
+}
+int io_d2h(uint8_t* h, const uint8_t* d, size_t n, hipStream_t s, IoRing& R, hipEvent_t ev[2]) {
+  if (!n) return 0;
+  if (!R.ok()) { HIPCHK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s)); HIPCHK(hipStreamSynchronize(s)); return 0; }
+  const size_t nk = (n + IO_CHUNK - 1) / IO_CHUNK;
+  auto chunk = [&](size_t k) { return std::min<size_t>(IO_CHUNK, n - k * IO_CHUNK); };
+  auto issue = [&](size_t k) -> int {
+    HIPCHK(hipMemcpyAsync(R.p[k & 1], d + k * IO_CHUNK, chunk(k), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(ev[k & 1], s));
+    return 0;
+  };
+  if (int r = issue(0)) return r;
+  for (size_t k = 0; k < nk; k++) {
+    if (k + 1 < nk) if (int r = issue(k + 1)) return r;
+    HIPCHK(hipEventSynchronize(ev[k & 1]));
+    par_memcpy(h + k * IO_CHUNK, R.p[k & 1], chunk(k));
+  }
+  return 0;
 }
 
 // Walks `nranges` ranges from `first`; on return wr (pinned) holds the
@@ -1004,6 +1121,7 @@ int plan_index_dev(zd_plan* P, const uint8_t* d_src, size_t n, hipStream_t s) {
   std::vector<HostPart> keep;
   int status = 0;
   double t_walk = 0, t_tail = 0;
+  uint64_t serial_dev = 0;                    // bytes the stitch walked itself (tail walks)
   if (n) {
     DevWalkBufs& B = dev_walk_bufs();
     std::lock_guard<std::mutex> lk(B.m);
@@ -1023,37 +1141,73 @@ int plan_index_dev(zd_plan* P, const uint8_t* d_src, size_t n, hipStream_t s) {
     if (int r = dev_walk(B, d_src, n, 0, chunk, T, s, &F, &NB, &fr, &bl)) return r;
     t_walk = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
     const auto cut = [&](size_t k) { return std::min<uint64_t>((uint64_t)k * chunk, n); };
+    struct Chain {                                   // one range's frames
+      const HostFrame* p; size_t n;
+      size_t size() const { return n; }
+      const HostFrame& operator[](size_t i) const { return p[i]; }
+    };
+    // the walk's results stay in the pinned buffers unless a tail walk (which
+    // reuses them) is needed: then they move to host vectors first
+    std::vector<WalkRange> wr_keep;
+    std::vector<HostFrame> fr_keep;
+    std::vector<HostBlock> bl_keep;
+    const WalkRange* wr = B.h_wr;
+    auto chain = [&](size_t k) { return Chain{fr + wr[k].f_off, wr[k].nframes}; };
     std::vector<const HostFrame*> kept;
     kept.reserve(F);
     size_t cur = 0;
-    bool tail = false;
-    for (size_t k = 0; k < T && !status; k++) {
-      const WalkRange& R = B.h_wr[k];
-      if (k && cur >= cut(k + 1)) continue;          // the range lies inside a kept frame
-      const HostFrame* rf = fr + R.f_off;
-      size_t i = 0;
-      while (i < R.nframes && rf[i].d.src_offset < cur) i++;
-      if (k && (i == R.nframes || rf[i].d.src_offset != cur)) { tail = true; break; }
-      for (; i < R.nframes; i++) kept.push_back(rf + i);
-      status = R.status;
-      cur = R.end;
+    for (size_t k = 0; k < T && !status;) {
+      const WalkRange& R = wr[k];
+      if (k && cur >= cut(k + 1)) { k++; continue; } // the range lies inside a kept frame
+      const Chain c = chain(k);
+      const size_t i0 = k ? chain_start(c, cur) : 0;
+      if (i0 != SIZE_MAX) {
+        for (size_t i = i0; i < c.n; i++) kept.push_back(c.p + i);
+        status = R.status;
+        cur = R.end;
+        k++;
+        continue;
+      }
+      // the chains do not meet: walk on from cur one range at a time on the
+      // device (frames that start before the range's end), until the chain
+      // reaches a frame start of a later range's chain (plan_index's rule)
+      const auto tt = std::chrono::steady_clock::now();
+      if (wr_keep.empty()) {
+        wr_keep.assign(B.h_wr, B.h_wr + T);
+        fr_keep.assign(fr, fr + F);
+        bl_keep.assign(bl, bl + NB);
+        wr = wr_keep.data(); fr = fr_keep.data(); bl = bl_keep.data();
+      }
+      parts_from(kept, bl, keep);                    // (kept may point into the pinned copy: same bytes)
+      kept.clear();
+      size_t kk = k;
+      for (;;) {
+        uint64_t F2 = 0, NB2 = 0;
+        const HostFrame* fr2 = nullptr;
+        const HostBlock* bl2 = nullptr;
+        const uint64_t hi = std::max<uint64_t>(cut(kk + 1), cur + 1);
+        if (int r = dev_walk(B, d_src, n, cur, hi - cur, 1, s, &F2, &NB2, &fr2, &bl2)) return r;
+        std::vector<const HostFrame*> t2;
+        for (uint64_t i = 0; i < F2; i++) t2.push_back(fr2 + i);
+        parts_from(t2, bl2, keep);
+        status = B.h_wr[0].status;
+        serial_dev += B.h_wr[0].end - cur;
+        cur = B.h_wr[0].end;
+        if (status || !F2 || cur >= n) break;
+        while (kk + 1 < T && cur >= cut(kk + 1)) kk++;
+        if (kk > k && chain_start(chain(kk), cur) != SIZE_MAX) break;
+      }
+      t_tail += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tt).count();
+      k = (kk > k && !status && cur < n) ? kk : T;
     }
     parts_from(kept, bl, keep);
-    if (tail) {                                      // the chains do not meet: the rest serially
-      const auto tt = std::chrono::steady_clock::now();
-      if (int r = dev_walk(B, d_src, n, cur, n - cur, 1, s, &F, &NB, &fr, &bl)) return r;
-      status = B.h_wr[0].status;
-      kept.clear();
-      for (uint64_t i = 0; i < F; i++) kept.push_back(fr + i);
-      parts_from(kept, bl, keep);
-      t_tail = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tt).count();
-    }
   }
   P->set_parts(std::move(keep));
   if (getenv("ZD_PLAN_TIMES"))
     fprintf(stderr, "zd device walk: %.2f ms (kernels + index download %.2f, serial tail %.2f)\n",
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count(), t_walk, t_tail);
   P->index_status = status;
+  P->info.walk_serial_bytes = serial_dev;
   P->index_stop = P->nframes;
   return 0;
 }
@@ -1088,7 +1242,7 @@ static void dump_plan_desc(const zd_plan* P) {
   w(at(W.jblkd, P->jblkd.data()), P->n_jblk * sizeof(JBlkDesc));
   w(at(W.jsegd, P->jsegd.data()), P->n_jseg * sizeof(JSegDesc));
   w(P->frame_out.data(), P->frame_out.size() * 8);
-  zd_plan_info I = P->info; I.workspace_bytes = 0; I.host_ns = I.device_ns = 0;
+  zd_plan_info I = P->info; I.workspace_bytes = 0; I.host_ns = I.device_ns = 0; I.walk_serial_bytes = 0;
   w(&I, sizeof I);
   uint64_t x[4] = {P->j_bytes, P->j_pieces, P->j_rounds, (uint64_t)(int64_t)P->index_status};
   w(x, sizeof x);
@@ -1141,7 +1295,23 @@ int zd_frames_index(const uint8_t* src, size_t n, zd_frame_desc* frames, size_t 
                     zd_block_desc* blocks, size_t cap_blocks, size_t* nblocks, size_t* consumed) {
   if (!src && n) return ZD_E_INVALID_ARG;
   zd_plan W;                                     // the host walk only (no device state)
-  plan_index(&W, src, n);
+  if (frames && cap_frames && cap_frames <= FRAMES_INDEX_SERIAL_MAX) {
+    // a few frames asked for: walk only those (serially), not the whole input
+    HostPart hp;
+    Bytes in{src, n};
+    for (size_t f = 0; f <= cap_frames && in.n; f++) {
+      HostFrame hf;
+      VecSink sink{hp.blocks};
+      const int r = index_frame(src, in, &hf, sink);
+      hp.frames.push_back(hf);
+      if (r) break;
+    }
+    std::vector<HostPart> v;
+    v.push_back(std::move(hp));
+    W.set_parts(std::move(v));
+  } else {
+    plan_index(&W, src, n);
+  }
   size_t nf = 0, nb = 0;
   int status = 0;
   size_t stop = n;
@@ -1173,6 +1343,32 @@ done:
   return status;
 }
 
+}  // extern "C"
+
+int zd::frame_spans(const uint8_t* src, size_t n, std::vector<uint64_t>& off, std::vector<uint64_t>& size,
+                    size_t* consumed) {
+  zd_plan W;
+  plan_index(&W, src, n);
+  off.clear();
+  size.clear();
+  off.reserve(W.nframes);
+  size.reserve(W.nframes);
+  size_t stop = n;
+  int status = 0;
+  for (const HostPart& hp : W.parts) {
+    for (const HostFrame& hf : hp.frames) {
+      if (hf.status) { status = hf.status; stop = (size_t)hf.d.src_offset; goto done; }
+      off.push_back(hf.d.src_offset);
+      size.push_back(hf.d.src_size);
+    }
+  }
+done:
+  if (consumed) *consumed = stop;
+  return status;
+}
+
+extern "C" {
+
 // zd_plan_create / zd_plan_create_device: the walk (host or device), then
 // the descriptors, the workspace and the upload.
 static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint32_t flags, hipStream_t s,
@@ -1199,7 +1395,7 @@ static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint3
             std::chrono::duration<double, std::milli>(t1 - ti).count());
   int r = upload_plan(P);
   const auto tu = std::chrono::steady_clock::now();
-  // the second stream and its events (K2 beside K3, opt-in overlap) exist
+  // the second stream and its events (K2 beside K3) exist
   // from here on, so zd_decode_async creates nothing
   if (!r && !aux_take(P)) r = ZD_E_HIP;
   if (r) { zd_plan_destroy(P); return r; }
@@ -1239,8 +1435,11 @@ void zd_plan_destroy(zd_plan* P) {
     (void)hipStreamSynchronize(P->last_stream);
     if (P->aux) (void)hipStreamSynchronize(P->aux);
   }
-  ws_release(P->d_ws, P->ws_bytes);
+  ws_release(P->d_ws, P->ws_bytes, P->dev);
   if (P->d_staging) (void)hipFree(P->d_staging);
+  if (P->d_meta) (void)hipFree(P->d_meta);
+  if (P->io_src) (void)hipFree(P->io_src);
+  if (P->io_dst) (void)hipFree(P->io_dst);
   if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
   aux_give(P);
   delete P;
@@ -1308,36 +1507,17 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   static const char* hops_env = getenv("ZD_J_HOPS");
   a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 8u;
   a.stream = s;
-  // the pipelined streaming executor K4P, opt-in (ZD_K4P=1, read per launch):
-  // parity-green but slower than K4 on C4
-  const char* k4p_env = getenv("ZD_K4P");
-  a.k4_pipe = k4p_env && atoi(k4p_env) != 0;
   // K3 as four lanes per block (K3Q, default): C3 (763 blocks) 2.89 -> 2.31
-  // ms, a forked 8,192-block plan 4.24 -> 2.48, full C4 13.88 -> 13.80;
-  // ZD_K3Q=0 (read per launch) keeps the one-lane chain
-  const char* k3q_env = getenv("ZD_K3Q");
-  a.k3_quad = !(k3q_env && atoi(k3q_env) == 0);
+  // ms, a forked 8,192-block plan 4.24 -> 2.48, full C4 13.88 -> 13.80; the
+  // plan flag ZD_F_SEQ_ONE_LANE keeps the one-lane chain (same records)
+  a.k3_quad = !(P->flags & ZD_F_SEQ_ONE_LANE);
   a.events = P->profile ? P->ev : nullptr;
-  if (const char* km = getenv("ZD_EXP_KMASK")) a.kmask = (uint32_t)strtoul(km, nullptr, 0);   // experiments only
   // K2 beside K3 on a second stream: slower where K3's rounds fill the LDS
   // (full C4: K3 is LDS-bound and K2 takes its CUs), faster where K3's last
-  // round leaves room (fork_auto); ZD_FORK=1 / 0 forces it on / off
+  // round leaves room (fork_auto); ZD_FORK=1 / 0 (read once) forces it on / off
   static const char* fork_env = getenv("ZD_FORK");
-  const bool fork = fork_env ? atoi(fork_env) == 1
-                             : fork_auto(P->n_seq);
-  static const bool overlap = getenv("ZD_OVERLAP") && atoi(getenv("ZD_OVERLAP")) == 1;
-  if (overlap && !fork && !P->staged && P->n_frames > 1) {
-    // K4 of the first half of the frames beside K3 of the second half
-    // (measured slower on C4, 45.1 vs 41.2 ms: both kernels are LDS-bound;
-    // plans small enough to keep host descriptors only)
-    a.overlap = true;
-    a.n_frames_a = (uint32_t)(P->n_frames / 2);
-    uint32_t k = 0;
-    while (k < P->list_seq.size() && P->comps[P->list_seq[k]].frame < a.n_frames_a) k++;
-    a.n_seq_a = k;
-  }
-  if (fork || a.overlap) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
-  if (const char* g = getenv("ZD_K4_GRID")) a.k4_grid = (uint32_t)strtoul(g, nullptr, 0);
+  const bool fork = fork_env ? atoi(fork_env) == 1 : fork_auto(P->n_seq);
+  if (fork) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
   HIPCHK(launch_pipeline(a));
   P->launched = true;
   P->last_stream = s;
@@ -1381,15 +1561,14 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
       HIPCHK(hipMemcpyAsync(tmp, d_dst, P->info.out_bytes, hipMemcpyDeviceToDevice, s));
       stage = tmp;
     }
-    uint64_t* d_meta = nullptr;
     size_t m = from.size();
-    HIPCHK(hipMalloc(&d_meta, 3 * m * sizeof(uint64_t)));
+    if (!grow_dev(P->d_meta, P->meta_cap, 3 * m)) return ZD_E_HIP;
+    uint64_t* d_meta = P->d_meta;
     HIPCHK(hipMemcpy(d_meta, from.data(), m * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_meta + m, to.data(), m * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_meta + 2 * m, len.data(), m * 8, hipMemcpyHostToDevice));
     HIPCHK(launch_compact(stage, d_dst, d_meta, d_meta + m, d_meta + 2 * m, (uint32_t)m, s));
     HIPCHK(hipStreamSynchronize(s));
-    (void)hipFree(d_meta);
     if (tmp) (void)hipFree(tmp);
   }
   if (first < 0 && P->index_status) { first = (int)nf; overall = P->index_status; }
@@ -1406,14 +1585,13 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
   const size_t nf = P->n_frames, m = P->res_off.size();   // frames 0..m-1 were decoded
   std::vector<uint64_t> h(m, 0);
   if (m) {
-    uint64_t* d = nullptr;
-    HIPCHK(hipMalloc(&d, 3 * m * sizeof(uint64_t)));
+    if (!grow_dev(P->d_meta, P->meta_cap, 3 * m)) return ZD_E_HIP;
+    uint64_t* d = P->d_meta;
     hipError_t e = hipMemcpy(d, P->res_off.data(), m * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d + m, P->res_len.data(), m * 8, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = launch_xxh64(d_dst, d, d + m, (uint32_t)m, d + 2 * m, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) e = hipMemcpy(h.data(), d + 2 * m, m * 8, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
     if (e != hipSuccess) return ZD_E_HIP;
   }
   for (size_t f = 0; f < nf; f++) {
@@ -1427,23 +1605,37 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
 
 int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
   if (!P || (!src && n) || n != P->info.src_bytes) return ZD_E_INVALID_ARG;
-  uint8_t *d_src = nullptr, *d_dst = nullptr;
-  uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
-  auto cleanup = [&]() { if (d_src) (void)hipFree(d_src); if (d_dst) (void)hipFree(d_dst); };
-  if (hipMalloc(&d_src, n + ZD_SRC_PADDING) != hipSuccess || hipMalloc(&d_dst, ob) != hipSuccess) {
-    cleanup(); return ZD_E_HIP;
-  }
-  if (n && hipMemcpy(d_src, src, n, hipMemcpyHostToDevice) != hipSuccess) { cleanup(); return ZD_E_HIP; }
-  int r = zd_decode_async(P, d_src, d_dst, ob, nullptr);
+  const uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
+  // device buffers owned by the plan (kept for the next call), the input and
+  // output through the pinned ring (chunked, the host copies on the worker
+  // pool overlapping the DMA), everything on one stream
+  if (!grow_dev(P->io_src, P->io_src_cap, n + ZD_SRC_PADDING) || !grow_dev(P->io_dst, P->io_dst_cap, ob))
+    return ZD_E_HIP;
+  const hipStream_t s = nullptr;
+  IoRing& R = io_ring();
+  std::lock_guard<std::mutex> lk(R.m);
+  IoEvents ev;
+  if (!ev.ok) return ZD_E_HIP;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (int r = io_h2d(P->io_src, src, n, s, R, ev.e)) return r;
+  HIPCHK(hipStreamSynchronize(s));
+  const auto t1 = std::chrono::steady_clock::now();
+  int r = zd_decode_async(P, P->io_src, P->io_dst, ob, s);
   uint64_t total = 0;
   int32_t first = -1;
-  if (!r) r = zd_plan_results(P, d_dst, nullptr, nullptr, nullptr, &total, &first);
-  if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG) { cleanup(); return r; }
-  int status = r;
-  size_t copy = (size_t)std::min<uint64_t>(total, cap);
-  if (copy && dst && hipMemcpy(dst, d_dst, copy, hipMemcpyDeviceToHost) != hipSuccess) { cleanup(); return ZD_E_HIP; }
+  if (!r) r = zd_plan_results(P, P->io_dst, s, nullptr, nullptr, &total, &first);
+  if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG || r == ZD_E_DST_TOO_SMALL) return r;
+  const int status = r;
+  const auto t2 = std::chrono::steady_clock::now();
+  const size_t copy = (size_t)std::min<uint64_t>(total, cap);
+  if (copy && dst)
+    if (int e = io_d2h(dst, P->io_dst, copy, s, R, ev.e)) return e;
+  const auto t3 = std::chrono::steady_clock::now();
+  auto ns = [](auto a, auto b) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count(); };
+  P->info.io_h2d_ns = ns(t0, t1);
+  P->info.io_decode_ns = ns(t1, t2);
+  P->info.io_d2h_ns = ns(t2, t3);
   if (out_len) *out_len = (size_t)total;
-  cleanup();
   if (!status && total > cap) return ZD_E_DST_TOO_SMALL;
   return status;
 }
@@ -1735,7 +1927,7 @@ int zd_block_decode(zd_context* c, const uint8_t* src, size_t n, size_t* consume
   }
   P.info.src_bytes = n;
   int r = ctx_run(c, &P, src, n);
-  ws_release(P.d_ws, P.ws_bytes);
+  ws_release(P.d_ws, P.ws_bytes, P.dev);
   P.d_ws = nullptr;
   if (P.d_staging) { (void)hipFree(P.d_staging); P.d_staging = nullptr; }
   return r;
@@ -1779,7 +1971,7 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   P.info.src_bytes = nlits;
   int r = upload_plan(&P);
   auto fin = [&](int rr) {
-    ws_release(P.d_ws, P.ws_bytes);
+    ws_release(P.d_ws, P.ws_bytes, P.dev);
     if (P.d_staging) (void)hipFree(P.d_staging);
     P.d_ws = nullptr; P.d_staging = nullptr;
     return rr;

@@ -921,22 +921,14 @@ constexpr int K3_LANES = ZD_K3_LANES;
 #define ZD_K3_WN 6                   // window dwords
 #endif
 #define K3_FAST seq_chainfl<ZD_K3_LA, ZD_K3_WN>
-#ifdef ZD_K3_EXACT
-#define K3_ENTRY(e, k, al) k3_entry(e, k)       // experiment: checks inside the chain (seq_chain2 on LDS)
-#else
 #define K3_ENTRY(e, k, al) k3f_entry(e, k, al)  // default: seq_chainfl, exact chain from HBM on a reject
-#endif
 constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
 static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
 
 __device__ inline void k3_store(uint64_t* p, uint32_t pos, uint32_t states) {
   const uint64_t v = (uint64_t)pos | ((uint64_t)states << 32);
-#ifdef ZD_K3_NT_STORE
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 template <typename TP, bool K3_SYM>
@@ -1136,11 +1128,7 @@ __device__ int seq_chainfl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, 
     const int32_t y = pos - use.wb;
     ymin = min(ymin, y);
     const uint32_t r = winn_at<N>(use, (uint32_t)y);
-#if defined(ZD_EXP_NOLOAD)
-    use.wb = pos - 100;                            // experiment: stale window bits, no load
-#else
     use = winn_load<N>(bs, m, pos);                // for the step L on
-#endif
     const uint32_t vO = __builtin_amdgcn_ubfe(r, 0, nbO), vM = __builtin_amdgcn_ubfe(r, nbO, nbM);
     const uint32_t vL = __builtin_amdgcn_ubfe(r, nbO + nbM, nbL);
     sLL = (nsL << nbL) + vL - TL;
@@ -1165,9 +1153,6 @@ __device__ int seq_chainfl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, 
   mx = max(mx, max(eLL, max(eML, eOF)));
   const uint32_t S = (__builtin_clz(eLL & 1023) + aL) + (__builtin_clz(eML & 1023) + aM) + (__builtin_clz(eOF & 1023) + aO);
   const int32_t E = (int32_t)((eLL >> 10) + (eML >> 10) + (eOF >> 10) - S);
-#if defined(ZD_EXP_NOLOAD)
-  ymin = 0;
-#endif
   return (mx >= K3F_BAD || ymin < 0 || pl < 0 || E > pl) ? 1 : 0;
 }
 
@@ -1235,21 +1220,11 @@ __global__ __launch_bounds__(K3_LANES) void zd_k_sequences(const uint8_t* __rest
   const uint8_t* blk = src + C.src;
   const uintptr_t lo = (uintptr_t)src;
   int st = 0;
-#ifdef ZD_K3_EXACT
-  if (use_lds)
-    st = K3_CHAIN<const lds_u16*, false>(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM,
-                                          al[0], al[1], al[2], C.nseq, recs + C.seq_out);
-  else
-#else
   bool exact = !use_lds;
   if (use_lds)
     exact = K3_FAST(blk + cs.bs_off, cs.bs_size, lo, mine, mine + K3_TL, mine + K3_TL + K3_TM, al[0], al[1],
                        al[2], C.nseq, recs + C.seq_out) != 0;
-#if defined(ZD_EXP_NOLOAD) || defined(ZD_EXP_NOSTORE)
-  exact = !use_lds;                               // experiments: garbage chains, no reruns
-#endif
   if (exact)
-#endif
     st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0],
                                  al[1], al[2], C.nseq, recs + C.seq_out);
   if (st) k3_fail(C, ci, cstate, fstate, st);
@@ -1489,22 +1464,11 @@ typedef __attribute__((address_space(3))) u32x4 l_u32x4;
 __device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
 // Match sources in HBM are read through the caches: the frame's own recent
 // output, re-read by later matches (nontemporal loads here: 28.3 -> 23.4 ms)
-#ifdef ZD_EXP_NOFAR
-// experiment: match sources "read" from the window instead of HBM (wrong bytes, timing only)
-__device__ inline u32x4 ldg16_nt(const uint8_t* p) {
-  return *(const __attribute__((address_space(3))) u32x4a1*)(((uintptr_t)p & 4095));
-}
-#else
 __device__ inline u32x4 ldg16_nt(const uint8_t* p) { return *(g_cu32x4a1*)p; }
-#endif
 // streams read once (records, literals): nontemporal, to leave the caches
 // to the frame outputs
 __device__ inline u32x4 ldg16_once(const uint8_t* p) {
-#ifdef ZD_K4_NT_STREAM
-  return __builtin_nontemporal_load((g_cu32x4a1*)p);
-#else
   return *(g_cu32x4a1*)p;
-#endif
 }
 __device__ inline u32x4 lds16(const l_u8* p) { return *(const l_u32x4a1*)p; }
 // stores the first n (0..16) bytes of v at p
@@ -1745,11 +1709,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
-#ifdef ZD_K4_STGFULL
-  __shared__ __attribute__((aligned(16))) uint8_t stg[1024 + 16];
-#else
   __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
-#endif
   const int lane = threadIdx.x;
 #if ZD_K4_CODELUT
   // LL | ML code -> baseline | extra-bit count << 24 (ll_code / ml_code,
@@ -1792,14 +1752,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   // HBM holds [0, fl_safe) with every store completed (the bytes two batches
   // back); fl_last = the flush boundary after the previous batch
   int32_t fl_safe = X.fl;
-#ifdef ZD_K4_LATE_FLUSH
-  int32_t fl_last = X.fl;
-#endif
 #ifdef ZD_K4_PROF
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memtime(), nb = 0, nr = 0;
-#define K4P(i) do { const uint64_t tn = __builtin_amdgcn_s_memtime(); ph[i] += tn - tq; tq = tn; } while (0)
+#define K4_PHASE(i) do { const uint64_t tn = __builtin_amdgcn_s_memtime(); ph[i] += tn - tq; tq = tn; } while (0)
 #else
-#define K4P(i) do { } while (0)
+#define K4_PHASE(i) do { } while (0)
 #endif
 
   for (uint32_t j = F.skip; j < F.nblocks && err_key == KEY_NONE; j++) {
@@ -1846,30 +1803,13 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     // for the window's room leaves the batch loop; the whole wave copies it
     // and the pipeline restarts after it.
     const bool lit_stage = lsrc != nullptr;
-#if defined(ZD_EXP_FIXVAL)
-    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? (uint64_t)i : 0; };
-#elif defined(ZD_K4_NT_STREAM)
-    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? __builtin_nontemporal_load(SQ + i) : 0; };
-#elif defined(ZD_EXP_HOTLOAD)
-    // experiment (timing only, wrong output): the streams' loads hit the first 64 records' lines
-    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? SQ[i & 63] : 0; };
-#else
     auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? SQ[i] : 0; };
-#endif
-#if defined(ZD_EXP_FIXVAL)
-    auto win_of = [&](uint64_t r, bool v) -> WinU { return WinU{r, r, 0}; };
-    auto lit_of = [&](uint32_t cur) -> u32x4 { return f4; };
-#elif defined(ZD_EXP_HOTLOAD)
-    auto win_of = [&](uint64_t r, bool v) -> WinU { return winu_load(bsp, (uintptr_t)src, 512 + 8 * lane); };
-    auto lit_of = [&](uint32_t cur) -> u32x4 { return lit_stage ? ldg16_once(lsrc + 16 * lane) : f4; };
-#else
     auto win_of = [&](uint64_t r, bool v) -> WinU {
       return winu_load(bsp, (uintptr_t)src, (v && !direct) ? (int32_t)(uint32_t)r : 0);
     };
     auto lit_of = [&](uint32_t cur) -> u32x4 {
       return (lit_stage && 16 * (uint32_t)lane < K4_STG && cur + 16 * (uint32_t)lane < nl) ? ldg16_once(lsrc + cur + 16 * lane) : f4;
     };
-#endif
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
       uint64_t recA = rec_at(s0 + lane), recB = rec_at(s0 + 64 + lane);
       WinU winA = win_of(recA, s0 + lane < n);
@@ -1880,41 +1820,27 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
       for (;;) {
         const uint32_t i = s0 + lane;
         const bool valid = i < n;
-        K4P(7);
-#ifdef ZD_K4_STGFULL
-        *(l_u32x4*)(stg + 16 * lane) = litA;
-#else
+        K4_PHASE(7);
         // this batch's literal bytes from the cursor on; lanes past the stage
         // all store into its 16-byte tail (only ever read as overshoot):
         // unconditional, a branch here cost 4 % of K4
         *(l_u32x4*)(stg + min(16 * (uint32_t)lane, K4_STG)) = litA;
-#endif
-#ifndef ZD_K4_LATE_FLUSH
         // The previous batch's output goes to HBM here, after the wait for
         // this batch's prefetched loads: those stores then have a batch to
         // drain before the next wait (vmcnt counts stores too, in order).
         // (the wait below is the one the compiler places here anyway)
         wait_vm();
         fl_safe = X.fl;
-#endif
         // the next batch's windows and the records after it, first thing
         const WinU winB = win_of(recB, s0 + 64 + lane < n);
         const uint64_t recC = rec_at(s0 + 128 + lane);
-#ifndef ZD_K4_LATE_FLUSH
         k4_flush(X, false);
-#endif
         // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
         // K3 recorded the bit position and the three states; OF, ML, LL
         // extra bits are read here, in that order, below the position.
         uint32_t ll = 0, ml = 0, ofv = 0;
         bool giant = false;
-#ifdef ZD_EXP_FIXVAL
-        // experiment (timing only, wrong output): fixed values, no stream data used
-        if (valid) { ll = 1; ml = 7; ofv = s0 == 0 ? 4 : 103 + (lane & 7); }
-        if (false) {
-#else
         if (valid) {
-#endif
           if (direct) {
             ll = seq_ll(recA); ml = seq_ml(recA); ofv = seq_off(recA);
             giant = ofv == DIRECT_GIANT;
@@ -1930,22 +1856,6 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
             ll_code(llc, &llbase, &llb);
             ml_code(mlc, &mlbase, &mlb);
 #endif
-#ifdef ZD_K4_V32
-            // the extra bits of a sequence usually fit the 32 bits below its
-            // position: three bit-field extracts on one funnel-shifted dword
-            // instead of 64-bit shifts; a batch with a wider lane takes the
-            // 64-bit path
-            const uint32_t E = ofc + mlb + llb;
-            if (__ballot(E > 32) == 0) {
-              const uint32_t k = winA.sh;              // top 32 bits below pos
-              const uint32_t hi = (uint32_t)(winA.w1 >> 32), lo = (uint32_t)winA.w1;
-              const uint32_t t32 = k == 0 ? hi : __builtin_amdgcn_alignbit(hi, lo, 32 - k);
-              const uint32_t o1 = 32 - ofc, o2 = o1 - mlb, o3 = o2 - llb;
-              ofv = (1u << ofc) + __builtin_amdgcn_ubfe(t32, o1, ofc);
-              ml = mlbase + __builtin_amdgcn_ubfe(t32, o2, mlb);
-              ll = llbase + __builtin_amdgcn_ubfe(t32, o3, llb);
-            } else
-#endif
             {
             uint64_t t = winu_top(winA, 0);
             const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
@@ -1955,7 +1865,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
             }
           }
         }
-        K4P(0);
+        K4_PHASE(0);
         // the next batch's literal bytes (used only when all 64 lanes
         // execute, so from the cursor after all of them)
         const uint32_t inc_ll = wave_scan_incl(ll);
@@ -2001,7 +1911,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           prev = ri;
           if (e) break;                                // the frame stops at this sequence
         }
-        K4P(1);
+        K4_PHASE(1);
         // matches whose source lies wholly in HBM, flushed two batches ago or
         // earlier (those stores completed before this batch's waits): their
         // first 32 source bytes are loaded now, to land during the checks
@@ -2055,30 +1965,16 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         const bool act = (uint32_t)lane < k;
         k4_sync();                               // staged literals visible
         // literals (every lane its own run; from the stage when it holds them)
-#ifdef ZD_EXP_NOLIT
-        if (false) {                              // experiment: no literal copies
-#else
         if (act && ll) {
-#endif
           l_u8* d = X.at(X.pos + (int32_t)opos);
-#ifdef ZD_K4_LITSPLIT
-          // lit_stage is uniform: one loop per source kind, no per-piece select
-          if (!lit_stage) {
-            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, f4, ll - x);
-          } else if (lpos + ll <= K4_STG) {
-            const l_u8* sp = (const l_u8*)stg + lpos;
-            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lds16(sp + x), ll - x);
-          } else {
-#else
           if (!lit_stage || lpos + ll <= K4_STG) {
             const l_u8* sp = (const l_u8*)stg + lpos;
             for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
           } else {
-#endif
             for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
           }
         }
-        K4P(2);
+        K4_PHASE(2);
         // far matches from the bytes loaded above (ml < off: no overlap);
         // the rest in frontier rounds
         if (far || inwin) {
@@ -2113,13 +2009,9 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           }
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
-#ifdef ZD_EXP_NOROUNDS
-        uint64_t done = ~0ull;                    // experiment: no near-match copies
-#else
         uint64_t done = __ballot(!act || ml == 0 || far || inwin);
-#endif
         k4_sync();
-        K4P(3);
+        K4_PHASE(3);
         while (done != ~0ull) {
           const int U = __ffsll((long long)~done) - 1;
           const int32_t qU = __builtin_amdgcn_readlane(q, U);
@@ -2145,7 +2037,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           nr++;
 #endif
         }
-        K4P(4);
+        K4_PHASE(4);
 #ifdef ZD_K4_PROF
         nb++;
 #endif
@@ -2153,18 +2045,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         lit_cursor += L;
         X.pos += (int32_t)T;
         s0 += k;
-#ifdef ZD_K4_LATE_FLUSH
-        fl_safe = fl_last;
-        fl_last = X.fl;
-        k4_flush(X, false);
-#endif
-        K4P(5);
+        K4_PHASE(5);
         if (k < 64 || s0 >= n) break;                  // a partial batch: the pipeline restarts at s0
         recA = recB; winA = winB; recB = recC; litA = litB;
       }
-#ifndef ZD_K4_LATE_FLUSH
       k4_flush(X, false);                            // k4_room and the large-sequence path expect it
-#endif
       if (big && err_key == KEY_NONE) {
         // one sequence larger than the window's room: the whole wave copies it
         if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, bll) ||
@@ -2193,410 +2078,6 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
            (unsigned long long)ph[2], (unsigned long long)ph[3], (unsigned long long)ph[4], (unsigned long long)ph[5],
            (unsigned long long)ph[7]);
 #endif
-  if (lane == 0) {
-    S->out_len = (uint64_t)X.pos;
-    S->rep[0] = rep[0];
-    S->rep[1] = rep[1];
-    S->rep[2] = rep[2];
-  }
-  k4_sync();                               // the window is reused by the next frame
-  }
-}
-
-// ---------------------------------------------------------------------------
-// K4P: the streaming execute as a two-stage software pipeline (default for
-// the frames K4 takes).  Same window, batches and copies as K4 above, but
-// the work of batch b is split:
-//   decode (stage D)  values from the K3 record, the bitstream window and
-//                     the block's symbols; scans; decode_offset; the
-//                     reference's checks in sequence order; the frame
-//                     position of every sequence; and the loads the copies
-//                     will need: the lane's first 16 literal bytes and, for
-//                     a match whose source was flushed to HBM, its first 16
-//                     source bytes
-//   copy (stage C)    literals, far matches from the loaded bytes, near
-//                     matches in frontier rounds (LDS), flush
-// and each iteration runs D of batch b + 1 before C of batch b, so every
-// load a copy consumes was issued a whole batch earlier (K4 issued its far
-// loads and waited for them inside one batch, and prefetched its streams
-// only one batch ahead: with stream data and copies removed, K4 took 1.8
-// ms of 8.4 on 4 GiB of C4; with the stream loads back, 4.7).  Records are
-// loaded two batches ahead, bitstream windows one.  The loop body is
-// unrolled by two with the two batches' registers in fixed roles, so no
-// register rotation waits on a load in flight.  A batch that does not fit
-// the window's room (a long sequence) ends the pipeline: it is executed on
-// its own (k < 64 lanes, or one sequence by the whole wave) and the
-// pipeline restarts after it.
-// ---------------------------------------------------------------------------
-struct K4Slot {            // one batch's stream data for stage D
-  uint64_t rec;            // the lane's K3 record
-  WinU win;                // the bitstream window at its position
-};
-#ifndef ZD_K4P_C
-#define ZD_K4P_C 3584
-#endif
-#ifndef ZD_K4P_W
-#define ZD_K4P_W 1024
-#endif
-#ifndef ZD_K4P_B
-#define ZD_K4P_B 1536
-#endif
-#ifndef ZD_K4P_MINW
-#define ZD_K4P_MINW 4
-#endif
-// K4P's window: 4 KiB (the copies' loaded bytes take 4 KiB of LDS DMA
-// buffers beside it; 16 waves per CU either way)
-typedef K4W<ZD_K4P_C, ZD_K4P_W, ZD_K4P_B> K4P;
-typedef __attribute__((address_space(3))) void l_void;
-typedef __attribute__((address_space(1))) const void g_cvoid;
-struct K4Dec {             // one decoded batch, per lane (its literal and far
-                           // source bytes wait in LDS: dma[parity])
-  uint32_t lm;             // ll | ml << 11 | far << 22 (a batch fits the room: ll + ml < 2^11)
-  uint32_t pos;            // opos | lpos << 11: output / literal offset of the lane's sequence in the batch
-  uint32_t off;            // < 2^31 (larger offsets fail the checks)
-};
-struct K4Bat {             // one decoded batch, uniform
-  uint32_t k;              // lanes executed (0: nothing decoded)
-  uint32_t T, L;           // output / literal bytes of the batch
-  uint32_t lit0;           // literal cursor at the batch start
-  int32_t p0;              // frame position at the batch start
-  uint32_t big;            // 1: one sequence for the whole wave (bll / bml / boff)
-  uint32_t bll, bml;
-  uint64_t boff;
-};
-
-__global__ __launch_bounds__(64, ZD_K4P_MINW) void zd_k_execute_pipe(const uint8_t* __restrict__ src, uint8_t* outbase,
-                                                        const FrameDesc* __restrict__ frames, FrameState* fstate,
-                                                        const BlockRec* __restrict__ blocks,
-                                                        const CompBlock* __restrict__ comp,
-                                                        const CompState* __restrict__ cstate,
-                                                        const uint8_t* __restrict__ lits,
-                                                        const uint64_t* __restrict__ seqs,
-                                                        const uint16_t* __restrict__ fses, uint32_t f_begin,
-                                                        uint32_t f_end) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[K4P::C];
-  __shared__ __attribute__((aligned(16))) uint8_t pat[64];
-  __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
-  // per batch parity, loaded by LDS DMA (global_load_lds) during the
-  // previous batch: the batch's first 1 KiB of literals, and 32 source
-  // bytes per far match
-  __shared__ __attribute__((aligned(16))) uint8_t dma[2][3][1024];
-  const int lane = threadIdx.x;
-  for (uint32_t f = f_begin + blockIdx.x; f < f_end; f += gridDim.x) {
-  const FrameDesc F = frames[f];
-  if (F.lds) continue;                           // K4F / K4J execute this frame
-  FrameState* S = &fstate[f];
-  const uint64_t key0 = S->key;
-  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) continue;
-
-  K4P X;
-  X.buf = (l_u8*)win;
-  X.out = outbase + F.out;
-  X.a0 = (int32_t)((16 - ((uintptr_t)X.out & 15)) & 15);
-  X.lane = lane;
-  X.pos = (int32_t)(F.out_len0 + F.skip_bytes);    // K0 wrote the leading raw/RLE blocks
-  X.fl = X.pos;
-  X.cap = (int32_t)(F.out_cap < 0x7FFFFFF0ull ? F.out_cap : 0x7FFFFFF0ull);
-  {
-    X.hs = X.alignd(X.pos > K4P::W ? X.pos - K4P::W : 0);
-    for (int32_t p = (X.hs > 0 ? X.hs : 0) + lane; p < X.pos; p += 64) *X.at(p) = X.out[p];
-    k4_sync();
-  }
-  uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
-  uint64_t err_key = KEY_NONE;
-
-  for (uint32_t j = F.skip; j < F.nblocks && err_key == KEY_NONE; j++) {
-    const BlockRec B = blocks[F.first_block + j];
-    if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
-    if (B.type == 5) continue;
-    if (B.type == 0 || B.type == 4) {
-      if (!k4_emit_lits(X, src + B.src, 0, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN);
-      continue;
-    }
-    if (B.type == 1) {
-      if (!k4_emit_lits(X, nullptr, B.rle, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN);
-      continue;
-    }
-    const CompBlock C = comp[B.comp];
-    const CompState CS = cstate[B.comp];
-    if (CS.stop) break;
-    const uint8_t* lsrc = nullptr;
-    uint32_t lfill = 0;
-    uint32_t nl;
-    if (C.lit_type == LIT_RAW) { lsrc = src + C.src + C.lit_data; nl = C.lit_regen; }
-    else if (C.lit_type == LIT_RLE) { lfill = C.lit_rle; nl = C.lit_regen; }
-    else { lsrc = lits + C.lit_out; nl = CS.lit_count; }
-    const u32x4 f4 = (u32x4){lfill * 0x01010101u, lfill * 0x01010101u, lfill * 0x01010101u, lfill * 0x01010101u};
-    const uint64_t* SQ = seqs + C.seq_out;
-    const uint32_t n = C.nseq;
-    const uint8_t* bsp = src + C.src + CS.bs_off;
-    if (n) {
-      for (int k = 0; k < 3; k++) {
-        const uint32_t s = (uint32_t)C.tab_src[k];
-        const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
-        const int cnt = 1 << cstate[s].al[k];
-        for (int e = lane; e < cnt; e += 64) stab[k][e] = (uint8_t)(g[e] & 63);
-      }
-      k4_sync();
-    }
-    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? SQ[i] : 0; };
-    auto win_of = [&](uint64_t r, bool v) -> WinU { return winu_load(bsp, (uintptr_t)src, v ? (int32_t)(uint32_t)r : 0); };
-
-    // decode side (uniform): the next batch to decode and where it lands
-    uint32_t s0d = 0;                 // first sequence not decoded yet
-    int32_t dpos = X.pos;             // frame position after the decoded batches
-    uint32_t dlit = 0;                // literal cursor after them
-    bool restart = false;             // the prefetched slots do not match s0d any more
-
-    // Stage D: decode the batch at s0d from slot `u` (its record and
-    // window), prefetch for the batches after it (`o`'s window: the next
-    // batch, whose record is loaded; `u`'s record: two batches on), and
-    // issue the loads the batch's copies need.  fsafe: the frame prefix
-    // whose HBM stores are complete.
-    auto decode = [&](K4Slot& u, K4Slot& o, K4Dec& d, K4Bat& bt, int32_t fsafe, l_u8* dl, l_u8* df, l_u8* df2) {
-      bt.k = 0; bt.big = 0;
-      if (s0d >= n || err_key != KEY_NONE) return;
-      const uint32_t i = s0d + lane;
-      const bool valid = i < n;
-      uint32_t ll = 0, ml = 0, ofv = 0;
-      if (valid) {
-        const uint32_t stt = (uint32_t)(u.rec >> 32);
-        const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
-        uint32_t llbase, llb, mlbase, mlb;
-        ll_code(llc, &llbase, &llb);
-        ml_code(mlc, &mlbase, &mlb);
-        uint64_t t = winu_top(u.win, 0);
-        const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
-        ofv = (1u << ofc) + ob;
-        ml = mlbase + mb;
-        ll = llbase + lb;
-      }
-      // the streams for the next two batches (their slots are free now)
-      o.win = win_of(o.rec, s0d + 64 + lane < n);
-      u.rec = rec_at(s0d + 128 + lane);
-      const uint32_t inc_ll = wave_scan_incl(ll);
-      const uint32_t tot = ll + ml;
-      const uint32_t inc_tot = wave_scan_incl(tot);
-      const uint32_t opos = inc_tot - tot, lpos = inc_ll - ll;
-      // lanes whose output fits the room k4_room keeps for a batch
-      const uint64_t fitm = __ballot(valid && (int64_t)inc_tot <= (int64_t)K4P::B - 16);
-      const uint32_t k = (uint32_t)__popcll(fitm);
-      const int kk = k ? (int)k : 1;
-      // decode_offset (decoding_context.rs:50-75): fresh offsets (> 3)
-      // direct, repeat codes walked in order on the scalar unit
-      const bool fresh = ofv > 3;
-      const uint64_t val = (uint64_t)ofv - 3;
-      uint64_t off = val;
-      int derr = 0;
-      uint64_t rm = __ballot(valid && !fresh && lane < kk);
-      uint64_t r0 = rep[0], r1 = rep[1], r2 = rep[2];
-      int prev = -1;
-      while (rm) {
-        const int ri = __ffsll((long long)rm) - 1;
-        rm &= rm - 1;
-        uint64_t a0, a1, a2;
-        rep_push(val, ri - prev - 1, ri, r0, r1, r2, &a0, &a1, &a2);
-        const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)ofv, ri);
-        const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)ll, ri);
-        uint64_t o2 = 0;
-        int e = 0;
-        if (oi == 0) {
-          e = ZD_E_NULL_OFFSET;
-        } else {
-          const uint32_t idx = oi - (li != 0 ? 1u : 0u);
-          if (idx == 0) { o2 = a0; }
-          else if (idx == 1) { o2 = a1; a1 = a0; a0 = o2; }
-          else if (idx == 2) { o2 = a2; a2 = a1; a1 = a0; a0 = o2; }
-          else if (a0 == 0) { e = ZD_E_REF_PANIC; }     // usize underflow of offsets[0] -= 1
-          else { o2 = a0 - 1; a2 = a1; a1 = a0; a0 = o2; }
-        }
-        if (lane == ri) { off = o2; derr = e; }
-        r0 = a0; r1 = a1; r2 = a2;
-        prev = ri;
-        if (e) break;                                // the frame stops at this sequence
-      }
-      // checks (decoding_context.rs:86-90, D9), first failing sequence
-      const uint64_t before = (uint64_t)dpos + opos;
-      const bool dbad = valid && derr != 0;
-      const bool imp = valid && !dbad && ((uint64_t)dlit + lpos + ll > nl || off > before + ll);
-      const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
-      const uint64_t badm = __ballot(dbad || imp || panic);
-      if (badm) {
-        const int b = __ffsll((long long)badm) - 1;
-        if (b < kk) {
-          const int code = __shfl(dbad ? derr : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
-          err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0d + b, code);
-          return;
-        }
-      }
-      bt.lit0 = dlit;
-      bt.p0 = dpos;
-      if (k == 0) {                                  // lane 0 alone does not fit the room
-        bt.big = 1;
-        bt.k = 1;
-        bt.bll = (uint32_t)__builtin_amdgcn_readlane((int)ll, 0);
-        bt.bml = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0);
-        bt.boff = readlane_u64(off, 0);
-        bt.T = bt.bll + bt.bml;
-        bt.L = bt.bll;
-        rep_push(val, 0 - prev, 1, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
-        if ((int64_t)dpos + bt.T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0d, ZD_E_OUT_OF_DOMAIN); return; }
-        dpos += (int32_t)bt.T;
-        dlit += bt.L;
-        s0d += 1;
-        restart = true;
-        return;
-      }
-      const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
-      const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
-      if ((int64_t)dpos + T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0d, ZD_E_OUT_OF_DOMAIN); return; }
-      rep_push(val, (int)k - 1 - prev, (int)k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);   // state after lane k - 1
-      // the copies' loads: 16 literal bytes from the lane's run, and the
-      // first 16 source bytes of a match whose source HBM holds (unused
-      // lanes load valid bytes of the run / frame start: fixed counts)
-      const bool act = (uint32_t)lane < k;
-      const uint32_t off32 = (uint32_t)(off < 0x7FFFFFFFull ? off : 0x7FFFFFFFull);
-      const int32_t q = dpos + (int32_t)(opos + ll);
-      const int32_t slo = q - (int32_t)off32;
-      const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
-      // far: the source is in HBM (flushed, stores complete) and not
-      // within the history the window is sure to hold at the batch's copy
-      // (a slide keeps >= W - 15 bytes before the batch start)
-      const bool far = act && ml && off32 >= 16 && off32 <= (uint32_t)q && shi <= fsafe &&
-                       slo < dpos - (K4P::W - 32);
-      // (the literal buffer ends at its block's literals + 16: the stage
-      // reads no further; far sources read past 16 bytes only when ml > 16)
-      if (lsrc)
-        __builtin_amdgcn_global_load_lds((g_cvoid*)(lsrc + min(dlit + 16 * (uint32_t)lane, nl)), (l_void*)dl, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((g_cvoid*)(X.out + (far ? slo : 0)), (l_void*)df, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((g_cvoid*)(X.out + (far && ml > 16 ? slo + 16 : 0)), (l_void*)df2, 16, 0, 0);
-      d.lm = act ? (ll | (ml << 11) | (far ? 1u << 22 : 0u)) : 0u;
-      d.pos = opos | (lpos << 11);
-      d.off = off32;
-      bt.k = k;
-      bt.T = T;
-      bt.L = L;
-      dpos += (int32_t)T;
-      dlit += L;
-      s0d += k;
-      if (k < 64 && s0d < n) restart = true;         // the slots were loaded for s0d + 64
-    };
-
-    // Stage C: execute a decoded batch into the window, flush.
-    auto copy = [&](K4Dec& d, K4Bat& bt, const l_u8* dl, const l_u8* df, const l_u8* df2) {
-      if (!bt.k) return;
-      if (bt.big) {
-        // one sequence larger than the window's room: the whole wave copies it
-        if (!k4_emit_lits(X, lsrc ? lsrc + bt.lit0 : nullptr, lfill, bt.bll) ||
-            !k4_emit_match(X, (l_u8*)pat, (uint32_t)(bt.boff < 0xFFFFFFFFull ? bt.boff : 0xFFFFFFFFull), bt.bml))
-          err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0d, ZD_E_OUT_OF_DOMAIN);
-        return;
-      }
-      k4_room(X);
-      const uint32_t ll = d.lm & 2047, ml = (d.lm >> 11) & 2047, off32 = d.off;
-      const uint32_t opos = d.pos & 2047, lpos = d.pos >> 11;
-      const int32_t q = X.pos + (int32_t)(opos + ll);
-      const int32_t slo = q - (int32_t)off32;
-      const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
-      const bool far = (d.lm >> 22) & 1;
-      // literals (every lane its own run)
-      if (ll) {
-        l_u8* dd = X.at(X.pos + (int32_t)opos);
-        if (!lsrc || lpos + ll <= 1024) {
-          for (uint32_t x = 0; x < ll; x += 16) sts_n(dd + x, lsrc ? lds16(dl + lpos + x) : f4, ll - x);
-        } else {
-          for (uint32_t x = 0; x < ll; x += 16) sts_n(dd + x, ldg16(lsrc + bt.lit0 + lpos + x), ll - x);
-        }
-      }
-      // far matches from the loaded bytes (ml <= off: no overlap)
-      if (far) {
-        l_u8* dd = X.at(q);
-        sts_n(dd, lds16(df + 16 * lane), ml);
-        if (ml > 16) sts_n(dd + 16, lds16(df2 + 16 * lane), ml - 16);
-        for (uint32_t x = 32; x < ml; x += 16)       // the rest of a long one (rare)
-          sts_n(dd + x, ldg16_nt(X.out + slo + x), ml - x);
-      }
-      // a near match reaching below the window reads HBM: the flush
-      // stores must have landed
-      if (__ballot(ml && !far && slo < X.hs)) wait_vm();
-      uint64_t done = __ballot(ml == 0 || far);
-      k4_sync();
-      while (done != ~0ull) {
-        const int U = __ffsll((long long)~done) - 1;
-        const int32_t qU = __builtin_amdgcn_readlane(q, U);
-        const bool mine = !((done >> lane) & 1) && (lane == U || shi <= qU);
-        if (mine) {
-          l_u8* dd = X.at(q);
-          if (off32 >= 16) {
-            for (uint32_t x = 0; x < ml; x += 16) sts_n(dd + x, X.src16(slo + (int32_t)x), ml - x);
-          } else {                                   // small period: first 16 bytes bytewise, then 16-byte steps
-            const uint32_t m16 = period16(off32);
-            const uint32_t head = ml < 16 ? ml : 16;
-            uint32_t r = 0;
-            for (uint32_t x = 0; x < head; x++) {
-              dd[x] = *X.at(slo + (int32_t)r);
-              r = r + 1 == off32 ? 0 : r + 1;
-            }
-            for (uint32_t x = 16; x < ml; x += 16) sts_n(dd + x, lds16(dd + x - m16), ml - x);
-          }
-        }
-        done |= __ballot(mine);
-        k4_sync();
-      }
-      X.pos += (int32_t)bt.T;
-      k4_flush(X, false);
-    };
-
-    K4Slot sA, sB;
-    K4Dec d0, d1;
-    K4Bat b0, b1;
-    b0.k = b1.k = 0;
-    while (s0d < n && err_key == KEY_NONE) {
-      // (re)start the pipeline at s0d: records of the first two batches,
-      // the first batch's window
-      restart = false;
-      sA.rec = rec_at(s0d + lane);
-      sB.rec = rec_at(s0d + 64 + lane);
-      sA.win = win_of(sA.rec, s0d + lane < n);
-      k4_flush(X, false);
-      wait_vm();
-      decode(sA, sB, d0, b0, X.fl, (l_u8*)dma[0][0], (l_u8*)dma[0][1], (l_u8*)dma[0][2]);
-      for (;;) {
-        // D of the next batch into (sB, d1, b1), C of the batch in d0
-        wait_vm();
-        if (!restart && err_key == KEY_NONE) decode(sB, sA, d1, b1, X.fl, (l_u8*)dma[1][0], (l_u8*)dma[1][1], (l_u8*)dma[1][2]);
-        else b1.k = 0;
-        if (err_key != KEY_NONE) break;
-        copy(d0, b0, (l_u8*)dma[0][0], (l_u8*)dma[0][1], (l_u8*)dma[0][2]);
-        b0.k = 0;
-        if (err_key != KEY_NONE || !b1.k) break;
-        // the same with the roles swapped
-        wait_vm();
-        if (!restart && err_key == KEY_NONE) decode(sA, sB, d0, b0, X.fl, (l_u8*)dma[0][0], (l_u8*)dma[0][1], (l_u8*)dma[0][2]);
-        else b0.k = 0;
-        if (err_key != KEY_NONE) break;
-        copy(d1, b1, (l_u8*)dma[1][0], (l_u8*)dma[1][1], (l_u8*)dma[1][2]);
-        b1.k = 0;
-        if (err_key != KEY_NONE || !b0.k) break;
-      }
-      if (err_key != KEY_NONE) break;
-      wait_vm();
-      copy(d0, b0, (l_u8*)dma[0][0], (l_u8*)dma[0][1], (l_u8*)dma[0][2]);                      // a batch decoded before a restart
-      b0.k = 0;
-      copy(d1, b1, (l_u8*)dma[1][0], (l_u8*)dma[1][1], (l_u8*)dma[1][2]);
-      b1.k = 0;
-    }
-    if (err_key != KEY_NONE) break;
-    k4_flush(X, false);
-    // leftover literals (decoding_context.rs:101-103)
-    if (dlit < nl && !k4_emit_lits(X, lsrc ? lsrc + dlit : nullptr, lfill, nl - dlit))
-      err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_OUT_OF_DOMAIN);
-  }
-  if (err_key != KEY_NONE) {
-    if (lane == 0) key_min(fstate, f, err_key);
-    continue;
-  }
-  k4_flush(X, true);
   if (lane == 0) {
     S->out_len = (uint64_t)X.pos;
     S->rep[0] = rep[0];
@@ -3707,14 +3188,14 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   hipStream_t s = a.stream;
   hipError_t e;
   if (a.events) if ((e = hipEventRecord(a.events[0], s)) != hipSuccess) return e;
-  if (a.n_copies && (a.kmask & 8))
+  if (a.n_copies)
     hipLaunchKernelGGL(zd_k_rawcopy, dim3(a.n_copies), dim3(256), 0, s, a.src, a.out,
                        (const CopyDesc*)(ws + W.copies));
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
   // K2 and K3 are independent once their tables exist: with the fork, K1's
   // Huffman half and K2 run on the aux stream beside K1's sequence half and
   // K3 (not when timing kernels one by one)
-  const bool fork = a.aux && !a.overlap && !a.events && a.n_huf && a.n_seq && (a.kmask & 6) == 6;
+  const bool fork = a.aux && !a.events && a.n_huf && a.n_seq;
   hipStream_t s2 = fork ? a.aux : s;
   if (fork) {
     if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
@@ -3726,7 +3207,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(pass_small, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses);
     hipLaunchKernelGGL(pass_big, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses);
   };
-  if (a.n_tables && (a.kmask & 1)) {
+  if (a.n_tables) {
     if (fork) {
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2);
       k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s);
@@ -3735,14 +3216,14 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     }
   }
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
-  if (a.n_huf && (a.kmask & 2))
+  if (a.n_huf)
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s2, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
   if (fork)
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   auto k3 = [&](uint32_t l0, uint32_t l1) {
-    if (l1 > l0 && (a.kmask & 4)) {
+    if (l1 > l0) {
       if (a.k3_quad)
         hipLaunchKernelGGL(zd_k_sequences_q, dim3((l1 - l0 + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, s, a.src,
                            comp, cstate, fstate, (const uint32_t*)(ws + W.list_seq) + l0, l1 - l0,
@@ -3755,36 +3236,22 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   };
   auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st) {
     const uint32_t n = f1 - f0;
-    if (n && a.n_frames > a.n_k4f && (a.kmask & 8))   // frames on the streaming K4 (K4F's exit at once)
-      hipLaunchKernelGGL(a.k4_pipe ? zd_k_execute_pipe : zd_k_execute, dim3(a.k4_grid && a.k4_grid < n ? a.k4_grid : n),
+    if (n && a.n_frames > a.n_k4f)   // frames on the streaming K4 (K4F's exit at once)
+      hipLaunchKernelGGL(zd_k_execute, dim3(n),
                          dim3(64), 0, st, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
                          (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1);
   };
-  // Overlap (opt-in, ZD_OVERLAP=1): K4 of the first frames on the aux
-  // stream beside K3 of the rest (their sequences come later in list_seq).
-  const bool overlap = a.aux && a.overlap && !a.events && !fork && a.n_frames_a && a.n_frames_a < a.n_frames;
-  if (overlap) {
-    k3(0, a.n_seq_a);
-    if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
-    k4(0, a.n_frames_a, a.aux);
-    if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
-    k3(a.n_seq_a, a.n_seq);
-    k4(a.n_frames_a, a.n_frames, s);
+  k3(0, a.n_seq);
+  if (fork)
     if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-  } else {
-    k3(0, a.n_seq);
-    if (fork)
-      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-    if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
-    k4(0, a.n_frames, s);
-  }
-  if (a.n_k4f && (a.kmask & 8))
+  if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
+  k4(0, a.n_frames, s);
+  if (a.n_k4f)
     hipLaunchKernelGGL(zd_k_execute_lds, dim3(a.n_k4f), dim3(K4F_T), 0, s, a.src, a.out, frames, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses, (const uint32_t*)(ws + W.list_k4f));
   if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;
-  if (a.n_jframes && (a.kmask & 8)) {
+  if (a.n_jframes) {
     auto* jframes = (const JFrame*)(ws + W.jframes);
     auto* jd = (const JBlkDesc*)(ws + W.jblkd);
     auto* jb = (JBlk*)(ws + W.jblk);

@@ -18,14 +18,9 @@ struct LaunchArgs {
   hipEvent_t* events;      // optional: N_KERNELS + 1 events recorded around the kernels
   hipStream_t aux = nullptr;   // optional second stream: K2 beside K3
   hipEvent_t fork = nullptr, join = nullptr;
-  uint32_t kmask = 0xF;    // kernels to launch (bit k = K(k+1)); experiments only
-  uint32_t k4_grid = 0;    // cap on K4 workgroups (persistent over frames); 0 = one per frame
-  bool overlap = false;    // K4 of frames [0, n_frames_a) on aux beside K3 of the rest
-  uint32_t n_frames_a = 0, n_seq_a = 0;   // list_seq[0, n_seq_a) = the blocks of those frames
   uint32_t n_jframes = 0, n_jblk = 0, n_jseg = 0;   // K4J frames / their blocks / scatter segments
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
-  bool k4_pipe = false;    // streaming frames: the pipelined K4P (K4 for the context API's direct records)
   bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block
   uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
 };

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/zd.h"
+#include "zd_internal.h"
 
 namespace {
 
@@ -81,7 +82,27 @@ struct zd_comm {
   ncclComm_t nc = nullptr;
   int world = 0, rank = 0;
   int64_t* d_meta = nullptr;       // world x 4 int64: status, first error frame, length, root capacity
+  // zd_decode_sharded's device buffers, grown as needed and kept between calls
+  uint8_t* d_src = nullptr;
+  uint64_t src_cap = 0;
+  uint8_t* d_out = nullptr;
+  uint64_t out_cap = 0;
 };
+
+namespace {
+
+// *p holds at least `need` bytes afterwards (grown by hipMalloc, contents dropped)
+bool grow(uint8_t*& p, uint64_t& cap, uint64_t need) {
+  if (need <= cap) return true;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  if (hipMalloc(&p, need) != hipSuccess) { (void)hipGetLastError(); return false; }
+  cap = need;
+  return true;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -109,17 +130,16 @@ int zd_shard_partition(const uint64_t* frame_bytes, size_t n, int world, size_t*
 int zd_shard_range(const uint8_t* src, size_t n, int rank, int world, uint64_t* src_begin, uint64_t* src_end,
                    uint64_t* frame_begin, uint64_t* frame_end) {
   if (world <= 0 || rank < 0 || rank >= world || (!src && n)) return ZD_E_INVALID_ARG;
-  size_t nf = 0, nb = 0, cons = 0;
-  // the size query walks the whole input: its status is the first failing frame's
-  const int st = zd_frames_index(src, n, nullptr, 0, &nf, nullptr, 0, &nb, &cons);
-  std::vector<zd_frame_desc> fr(std::max<size_t>(nf, 1));
-  zd_frames_index(src, n, fr.data(), nf, &nf, nullptr, 0, &nb, &cons);
-  std::vector<uint64_t> sizes(nf);
-  for (size_t i = 0; i < nf; i++) sizes[i] = fr[i].src_size;
+  // one walk of the input (zd_frames_index's): the frames before the first
+  // that fails to index
+  std::vector<uint64_t> off, sizes;
+  size_t cons = 0;
+  const int st = zd::frame_spans(src, n, off, sizes, &cons);
+  const size_t nf = off.size();
   std::vector<size_t> cuts((size_t)world + 1);
   zd_shard_partition(sizes.data(), nf, world, cuts.data());
   const size_t b = cuts[(size_t)rank], e = cuts[(size_t)rank + 1];
-  auto off_of = [&](size_t f) -> uint64_t { return f < nf ? fr[f].src_offset : (uint64_t)cons; };
+  auto off_of = [&](size_t f) -> uint64_t { return f < nf ? off[f] : (uint64_t)cons; };
   uint64_t sb = off_of(b), se = off_of(e);
   // a frame that fails to index, and everything after it, goes to the last
   // rank: its plan stops there with that frame's status (FrameIterator)
@@ -164,7 +184,32 @@ void zd_comm_destroy(zd_comm* c) {
   Rccl* R = rccl();
   if (c->nc && R) R->CommDestroy(c->nc);
   if (c->d_meta) (void)hipFree(c->d_meta);
+  if (c->d_src) (void)hipFree(c->d_src);
+  if (c->d_out) (void)hipFree(c->d_out);
   delete c;
+}
+
+int zd_gather_layout(const int64_t* meta, int world, uint64_t* off, uint64_t* len, zd_gather_result* res) {
+  if (!meta || world <= 0 || !off || !len || !res) return ZD_E_INVALID_ARG;
+  // the output stops at the first failing rank's failure (src/main.rs:43-53)
+  int failed = world;
+  for (int r = 0; r < world; r++)
+    if (meta[4 * r] != 0) { failed = r; break; }
+  uint64_t total = 0;
+  for (int r = 0; r < world; r++) {
+    len[r] = (r <= failed && meta[4 * r + 2] > 0) ? (uint64_t)meta[4 * r + 2] : 0;
+    off[r] = total;
+    total += len[r];
+  }
+  res->total_len = total;
+  res->failed_rank = failed;
+  res->status = failed < world ? (int32_t)meta[4 * failed] : ZD_OK;
+  res->first_error_frame = failed < world ? meta[4 * failed + 1] : -1;
+  if (total > (uint64_t)std::max<int64_t>(meta[3], 0)) {   // rank 0's capacity, known to all
+    res->total_len = 0;
+    return ZD_E_DST_TOO_SMALL;
+  }
+  return ZD_OK;
 }
 
 int zd_comm_gather(zd_comm* c, const uint8_t* d_local, uint64_t local_len, int32_t status, int64_t first_error_frame,
@@ -182,25 +227,8 @@ int zd_comm_gather(zd_comm* c, const uint8_t* d_local, uint64_t local_len, int32
   std::vector<int64_t> m(4 * (size_t)W);
   HIPCHK(hipMemcpyAsync(m.data(), c->d_meta, sizeof(int64_t) * m.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  // the output stops at the first failing rank's failure (src/main.rs:43-53)
-  int failed = W;
-  for (int r = 0; r < W; r++)
-    if (m[4 * r] != 0) { failed = r; break; }
   std::vector<uint64_t> len((size_t)W, 0), off((size_t)W, 0);
-  uint64_t total = 0;
-  for (int r = 0; r < W; r++) {
-    len[r] = r <= failed ? (uint64_t)m[4 * r + 2] : 0;
-    off[r] = total;
-    total += len[r];
-  }
-  res->total_len = total;
-  res->failed_rank = failed;
-  res->status = failed < W ? (int32_t)m[4 * failed] : ZD_OK;
-  res->first_error_frame = failed < W ? m[4 * failed + 1] : -1;
-  if (total > (uint64_t)m[3]) {                 // rank 0's capacity, known to all: nobody sends
-    res->total_len = 0;
-    return ZD_E_DST_TOO_SMALL;
-  }
+  if (int r = zd_gather_layout(m.data(), W, off.data(), len.data(), res)) return r;   // nobody sends
   if (c->rank == 0 && len[0] && d_local != d_root_out)
     HIPCHK(hipMemcpyAsync(d_root_out, d_local, len[0], hipMemcpyDeviceToDevice, s));
   // point-to-point over the peers' own xGMI links to GPU 0
@@ -224,7 +252,7 @@ int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, 
   int32_t status = ZD_OK;
   int32_t first = -1;
   uint64_t len = 0;
-  uint8_t *d_src = nullptr, *d_out = nullptr;
+  uint8_t* d_out = nullptr;
   zd_plan* P = nullptr;
   // a local failure still takes part in the collective (as this rank's
   // status), so no rank is left waiting in it
@@ -237,10 +265,13 @@ int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, 
       const uint64_t ob = std::max<uint64_t>(info.out_bytes, 16);
       // rank 0's range comes first in the output: it decodes in place
       d_out = (c->rank == 0 && root_cap >= ob) ? d_root_out : nullptr;
-      if (hipMalloc(&d_src, se - sb + ZD_SRC_PADDING) != hipSuccess) { err = ZD_E_HIP; break; }
-      if (!d_out && hipMalloc(&d_out, ob) != hipSuccess) { d_out = nullptr; err = ZD_E_HIP; break; }
-      if (hipMemcpyAsync(d_src, src + sb, se - sb, hipMemcpyHostToDevice, s) != hipSuccess) { err = ZD_E_HIP; break; }
-      if ((err = zd_decode_async(P, d_src, d_out, ob, s))) break;
+      if (!grow(c->d_src, c->src_cap, se - sb + ZD_SRC_PADDING)) { err = ZD_E_HIP; break; }
+      if (!d_out) {
+        if (!grow(c->d_out, c->out_cap, ob)) { err = ZD_E_HIP; break; }
+        d_out = c->d_out;
+      }
+      if (hipMemcpyAsync(c->d_src, src + sb, se - sb, hipMemcpyHostToDevice, s) != hipSuccess) { err = ZD_E_HIP; break; }
+      if ((err = zd_decode_async(P, c->d_src, d_out, ob, s))) break;
       const int r = zd_plan_results(P, d_out, s, nullptr, nullptr, &len, &first);
       if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG) { err = r; break; }
       status = r;
@@ -248,8 +279,6 @@ int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, 
     if (err) { status = err; len = 0; first = 0; }
   }
   auto fin = [&](int r) {
-    if (d_src) (void)hipFree(d_src);
-    if (d_out && d_out != d_root_out) (void)hipFree(d_out);
     zd_plan_destroy(P);
     return r;
   };

@@ -43,7 +43,8 @@ class PlanInfo(C.Structure):
                 ("src_bytes", C.c_uint64), ("out_bytes", C.c_uint64), ("out_exact", C.c_uint64),
                 ("workspace_bytes", C.c_uint64), ("nsequences", C.c_uint64), ("nliterals", C.c_uint64),
                 ("index_status", C.c_int32), ("_pad", C.c_uint32), ("host_ns", C.c_uint64),
-                ("device_ns", C.c_uint64)]
+                ("device_ns", C.c_uint64), ("walk_serial_bytes", C.c_uint64),
+                ("io_h2d_ns", C.c_uint64), ("io_decode_ns", C.c_uint64), ("io_d2h_ns", C.c_uint64)]
 
 
 class GatherResult(C.Structure):
@@ -85,6 +86,8 @@ SIGNATURES = {
     "zd_comm_unique_id": (C.c_int, [_vp]),
     "zd_comm_create": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_vp)]),
     "zd_comm_destroy": (None, [_vp]),
+    "zd_gather_layout": (C.c_int, [C.POINTER(C.c_int64), C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                   C.POINTER(GatherResult)]),
     "zd_comm_gather": (C.c_int, [_vp, _vp, C.c_uint64, C.c_int32, C.c_int64, _vp, C.c_uint64,
                                  C.POINTER(GatherResult), _vp]),
     "zd_decode_sharded": (C.c_int, [_vp, _vp, _sz, C.c_uint32, _vp, C.c_uint64, C.POINTER(GatherResult), _vp]),
@@ -93,22 +96,38 @@ SIGNATURES = {
 _lib = None
 
 
+def _one_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64
+    (soname libamdhip64.so.7, loaded as torch/lib/libamdhip64.so), and libzd's
+    dependency on libamdhip64.so.7 binds to whichever copy is loaded first;
+    loading libzd before torch would leave torch a second runtime that finds
+    no GPU.  So torch's copy goes in first -- by path, without importing torch
+    (which costs seconds): a later `import torch` then maps the same file and
+    shares it.  With no torch installed, libzd takes ROCm's own runtime."""
+    import sys
+    if "torch" in sys.modules:
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        rt = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(rt):
+            C.CDLL(rt, mode=C.RTLD_GLOBAL)
+            return
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C zstd-decompressor_amd` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
-        # One HIP runtime per process: PyTorch-ROCm ships its own
-        # libamdhip64 (soname libamdhip64.so.7, loaded as "libamdhip64.so"),
-        # and libzd's dependency on libamdhip64.so.7 binds to whichever copy
-        # is already loaded.  Loading PyTorch's first keeps device pointers,
-        # streams and graphs from torch valid in libzd; loading libzd first
-        # would leave torch a second runtime that finds no GPU.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        _one_hip_runtime()
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
@@ -155,3 +174,4 @@ REF_PANIC, OUT_OF_DOMAIN, DST_TOO_SMALL, INVALID_ARG, HIP, NO_MEMORY, NOT_DECODE
 F_SKIPPABLE = 1
 F_BLOCK_PARALLEL = 2   # every frame with a compressed block -> K4J (block-parallel execute)
 F_FRAME_SERIAL = 4     # no frame -> K4J
+F_SEQ_ONE_LANE = 8     # K3 one lane per block instead of four (K3Q)
