@@ -191,6 +191,63 @@ def cpu_libzstd(frame_set: bytes, sample, threads: int):
                       f"{L.ZSTD_versionNumber()} ZSTD_decompress on {threads} host threads, {dt:.2f} s"}
 
 
+plan_io_scratch = []
+
+
+def host_io_leg(plan, data: bytes, info, src, reps: int):
+    """zd_plan_decompress (host in, host out; the INTEGRATION.md decompress())
+    on the bench plan: two warm calls, then the best of two timed, phase
+    times from zd_plan_info io_*_ns; the output checked against the source.
+    Plus the same on the reference's moby-dick sample (one small frame:
+    latency, not bandwidth).  Reported apart from value (PCIe-inclusive)."""
+    import ctypes as C
+    from zstd_decompressor import _lib
+    L = _lib.lib()
+    cap = int(info.out_bytes)
+    out = np.empty(cap + 64, dtype=np.uint8)
+    plan_io_scratch.append(out)
+    p, n, keep = _lib.buf(data)
+    ol = C.c_size_t()
+    best = None
+    for it in range(4):
+        t0 = time.time()
+        st = L.zd_plan_decompress(plan._h, p, n, C.c_void_p(out.ctypes.data), cap, C.byref(ol))
+        dt = time.time() - t0
+        pi = _lib.PlanInfo()
+        L.zd_plan_info_get(plan._h, C.byref(pi))
+        if st != 0 or ol.value != cap:
+            return {"error": f"zd_plan_decompress status {st}, {ol.value} of {cap} bytes"}
+        if it >= 2 and (best is None or dt < best[0]):
+            best = (dt, pi.io_h2d_ns / 1e6, pi.io_decode_ns / 1e6, pi.io_d2h_ns / 1e6)
+    ok = None
+    if src is not None:
+        u = len(src)
+        mv = memoryview(out)
+        ok = all(mv[r * u:(r + 1) * u] == src for r in range(reps))
+    dt, h2d, dec, d2h = best
+    res = {"MBps": round(cap / dt / 1e6, 1), "wall_ms": round(dt * 1e3, 2), "h2d_ms": round(h2d, 2),
+           "h2d_GBps": round(n / (h2d / 1e3) / 1e9, 1), "decode_ms": round(dec, 2), "d2h_ms": round(d2h, 2),
+           "d2h_GBps": round(cap / (d2h / 1e3) / 1e9, 1), "verified_bit_exact": ok,
+           "via": "zd_plan_decompress: pinned 32 MiB chunks, host copies on the worker pool, plan-owned device buffers"}
+    # the reference's own sample, host in / host out
+    from zstd_decompressor.batch import Plan
+    md = open(os.path.join(ROOT, "tests", "golden", "resources", "moby-dick.txt.zst"), "rb").read()
+    mp = Plan(md)
+    mcap = int(mp.info.out_bytes)
+    mout = np.empty(mcap + 64, dtype=np.uint8)
+    mpp, mn, mkeep = _lib.buf(md)
+    times = []
+    for it in range(12):
+        t0 = time.time()
+        st = L.zd_plan_decompress(mp._h, mpp, mn, C.c_void_p(mout.ctypes.data), mcap, C.byref(ol))
+        times.append(time.time() - t0)
+    mp.close()
+    tm = float(np.median(times[2:]))
+    res["moby_dick"] = {"MBps": round(mcap / tm / 1e6, 1), "wall_ms": round(tm * 1e3, 3), "status": int(st),
+                        "bytes": mcap}
+    return res
+
+
 def traffic_of(kernel: str, args, world: int):
     """HBM bytes per launch of `kernel` (FETCH_SIZE + WRITE_SIZE, rocprofv3
     --pmc passes of scripts/full_run.sh on the default 1-GPU workload, kept
@@ -428,6 +485,17 @@ def main():
         del root
         comm.close()
 
+    # ---- the drop-in's host-in / host-out path (never part of value) ----
+    # zd_plan_decompress on the same plan: input host -> HBM and output HBM ->
+    # host through pinned chunks, plan-owned device buffers (rank 0 only, the
+    # other ranks wait: one PCIe link measured alone)
+    host_io = None
+    if rank == 0 and not args.experiment:
+        host_io = host_io_leg(plan, data, info, src if not strong else ref_bytes, reps if not strong else 1)
+        del plan_io_scratch[:]
+    if dist:
+        dist.barrier()
+
     value = total_out.item() / (ms_per_step / 1e3) / 1e6
     alg_per_launch = out_bytes + comp_bytes          # C + D, this rank's launch
     dom_ms = kt[dom]
@@ -500,6 +568,9 @@ def main():
             "host_plan_split_ms": {"headers_and_descriptors": round(info.host_ns / 1e6, 1),
                                    "workspace_alloc_and_upload": round(info.device_ns / 1e6, 1)},
             "value_incl_host_plan": round(total_out.item() / (ms_per_step / 1e3 + host_plan_s) / 1e6, 1),
+            "h2d_ms": None if not host_io else host_io["h2d_ms"],
+            "d2h_ms": None if not host_io else host_io["d2h_ms"],
+            "host_io": host_io,
             "cpu_baseline": cpu,
             "cpu_libzstd": cpu_zstd,
             "verified_bit_exact": verified,

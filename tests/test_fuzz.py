@@ -49,6 +49,15 @@ def _mutate(r: random.Random, seeds):
     return bytes(d)
 
 
+def _dump_ood(data, p, tag):
+    """ZD_FUZZ_DUMP=DIR keeps every input that left the GPU path's domain."""
+    d = os.environ.get("ZD_FUZZ_DUMP")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{tag}_p{int(p)}.zst"), "wb") as f:
+            f.write(data)
+
+
 def test_fuzz_structure_aware():
     """ZD_FUZZ_ITERS / ZD_FUZZ_SEED run longer campaigns (default: 600 inputs)."""
     from zstd_decompressor.batch import decompress_status
@@ -63,10 +72,12 @@ def test_fuzz_structure_aware():
         gst, gout = decompress_status(data, p)
         if gst == OUT_OF_DOMAIN:
             seen["ood"] += 1
+            _dump_ood(data, p, f"s{it}")
             continue
         assert gst == ost, f"#{it}: oracle {ost}, gpu {gst}"
         assert gout == oout, f"#{it}: output differs"
         seen["ok" if ost == 0 else "err"] += 1
+    print("fuzz outcome counts:", seen)
     assert seen["ood"] <= max(30, iters // 10), seen
 
 
@@ -93,10 +104,12 @@ def test_fuzz_forked_plans():
         gst, gout = decompress_status(data, p)
         if gst == OUT_OF_DOMAIN:
             seen["ood"] += 1
+            _dump_ood(data, p, f"plan{it}")
             continue
         assert gst == ost, f"#{it}: oracle {ost}, gpu {gst}"
         assert gout == oout, f"#{it}: output differs"
         seen["ok" if ost == 0 else "err"] += 1
+    print("fuzz outcome counts (plans):", seen)
     assert seen["ood"] <= max(8, iters // 10), seen
 
 

@@ -96,10 +96,19 @@ ZD_HD inline uint32_t k3f_entry(uint32_t e, int k, int al) {
 }
 
 // ---------------------------------------------------------------------------
-// Sequence records (K3 -> K4), 8 bytes each:
-//   from K3 (FSE chain): low 32 bits = bit position of the sequence's extra
-//     bits (their top, before OF/ML/LL are read), high 32 bits = LL | ML << 10
-//     | OF << 20 states; K4 decodes the values (decoders/sequence.rs:41-55).
+// Sequence records (K3 -> K4), 8 bytes per sequence:
+//   from K3 (FSE chain): for each sequence the bit position of its extra
+//     bits (their top, before OF/ML/LL are read) and the LL / ML / OF states;
+//     K4 decodes the values (decoders/sequence.rs:41-55).  They come in pairs,
+//     sequences 2p and 2p + 1 in 16 bytes (a block's first record index is
+//     even), four dwords each written by one lane of K3Q's quad (OF | ML | LL
+//     | shadow) with no cross-lane moves:
+//       x  OF state of 2p | OF state of 2p+1 << 10 | (pos_2p - pos_2p+1) << 20
+//       y  ML states (bits 0-9, 10-19)       z  LL states
+//       w  pos_2p
+//     (a step reads at most 89 bits, so the position difference fits 12 bits;
+//     states are below 2^9).  rec_unpack gives one record of a pair in the
+//     consumers' one-word form: pos | (LL | ML << 10 | OF << 20) << 32.
 //   direct (zd_execute_sequences, CompBlock::seq_direct): bits 0-16
 //     literals_length, 17-34 match_length, 35-63 offset_value, where
 //     DIRECT_GIANT stands for any offset_value >= 2^29 - 1 (an offset past
@@ -107,6 +116,22 @@ ZD_HD inline uint32_t k3f_entry(uint32_t e, int k, int al) {
 // Repeat offsets (decoding_context.rs:50-75) are resolved by K4 in frame
 // order with concrete values.
 // ---------------------------------------------------------------------------
+ZD_HD inline uint64_t rec_unpack(uint32_t x, uint32_t y, uint32_t z, uint32_t w, uint32_t h) {
+  const uint32_t sh = 10 * h;
+  const uint32_t st = ((z >> sh) & 1023) | (((y >> sh) & 1023) << 10) | (((x >> sh) & 1023) << 20);
+  const uint32_t pos = h ? w - (x >> 20) : w;
+  return (uint64_t)pos | ((uint64_t)st << 32);
+}
+// the pair of records (posA, stA), (posB, stB) -- st = LL | ML << 10 | OF << 20
+ZD_HD inline void rec_pack(uint32_t posA, uint32_t stA, uint32_t posB, uint32_t stB, uint32_t v[4]) {
+  v[0] = (stA >> 20) | ((stB >> 20) << 10) | ((posA - posB) << 20);
+  v[1] = ((stA >> 10) & 1023) | (((stB >> 10) & 1023) << 10);
+  v[2] = (stA & 1023) | ((stB & 1023) << 10);
+  v[3] = posA;
+}
+// record slots a block of n sequences takes (pairs, and one spare pair that
+// the chains write past the last)
+ZD_HD inline uint64_t rec_slots(uint32_t n) { return n ? ((uint64_t)(n + 1) & ~1ull) + 2 : 0; }
 constexpr uint32_t DIRECT_GIANT = (1u << 29) - 1;
 // Output bounds per executor: the streaming K4 keeps int32 frame positions,
 // K4J 31-bit ones in its state words; a frame with sequences above both is

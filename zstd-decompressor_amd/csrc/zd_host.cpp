@@ -248,7 +248,7 @@ void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks,
       }
       cb.seq_out = c.nrec;
       c.nseq += cb.nseq;
-      c.nrec += cb.nseq + (cb.nseq ? 2 : 0);     // K3 writes up to two spare records past the block's last
+      c.nrec += rec_slots(cb.nseq);              // record pairs, a spare pair past the block's last
       seqs_in_frame |= cb.nseq > 0;
       br.comp = (int32_t)ci;
       jseg += cb.nseq > J_SEG ? (cb.nseq + J_SEG - 1) / J_SEG : 1;

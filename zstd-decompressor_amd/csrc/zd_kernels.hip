@@ -550,6 +550,9 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef __attribute__((address_space(1))) const u32x4a4 g_u32x4a4;   // global (HBM) window loads
 typedef __attribute__((address_space(3))) uint16_t lds_u16;          // LDS tables
 typedef __attribute__((address_space(1))) const uint16_t g_u16;      // HBM tables
+typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4g g_u32x4g;            // record pairs (16-byte aligned)
+typedef __attribute__((address_space(1))) uint32_t g_u32;
 
 // MSB-first field of k bits from the top of t, k in [0, 63], no selects:
 // (t >> 1) >> (63 - k) is 0 for k = 0.
@@ -926,9 +929,22 @@ constexpr int K3_TL = 512, K3_TM = 512, K3_TO = 256;
 constexpr int K3_TAB = K3_TL + K3_TM + K3_TO;
 static_assert(K3_LANES <= 64, "K3 workgroup must be a single wave");
 
-__device__ inline void k3_store(uint64_t* p, uint32_t pos, uint32_t states) {
-  const uint64_t v = (uint64_t)pos | ((uint64_t)states << 32);
-  *p = v;
+// records (posA, stA), (posB, stB) as a pair (zd_common.h rec_pack) at p
+__device__ inline void k3_store_pair(uint64_t* p, uint32_t posA, uint32_t stA, uint32_t posB, uint32_t stB) {
+  uint32_t v[4];
+  rec_pack(posA, stA, posB, stB, v);
+  *(g_u32x4g*)p = u32x4g{v[0], v[1], v[2], v[3]};
+}
+// record i of a block (K3's pairs, zd_common.h, or a direct word)
+__device__ inline uint64_t rec_get(const uint64_t* SQ, uint32_t i, bool direct) {
+  if (direct) return SQ[i];
+  const u32x4g v = *(const g_u32x4g*)(SQ + (i & ~1u));
+  return rec_unpack(v.x, v.y, v.z, v.w, i & 1);
+}
+// record j of the block's pairs, read back after the chain stored it
+__device__ inline uint64_t k3_reread(const uint64_t* out, uint32_t j) {
+  const u32x4g v = *(volatile g_u32x4g*)(out + (j & ~1u));
+  return rec_unpack(v.x, v.y, v.z, v.w, j & 1);
 }
 
 template <typename TP, bool K3_SYM>
@@ -949,22 +965,22 @@ __device__ int seq_chain2(const uint8_t* bs, uint32_t bs_size, uintptr_t base, T
   const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
   const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
   // The loop entry sees the same memory-op order as its back edge (window,
-  // store, window, store), so the wait for a window two steps old is
-  // vmcnt(4), not a drain: step 0's window is loaded again for that.
+  // store, window), so the wait for a window two steps old is not a drain:
+  // step 0's window is loaded again for that.  Records are stored in pairs
+  // (zd_common.h): the even step of an iteration stores (record i, record
+  // i + 1), the odd one keeps its record for the next pair.
   Win6 wa = win6_load(bs, m, pos0);              // step 0 (covers pos0 - A - 90)
   asm volatile("" ::: "memory");
-  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+  uint32_t pPos = (uint32_t)pos, pSt = sLL | (sML << 10) | (sOF << 20);   // record 0
+  k3_store_pair(out, pPos, pSt, pPos, pSt);
   Win6 wb = win6_load(bs, m, pos);               // step 1
-  asm volatile("" ::: "memory");
-  k3_store(out, (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
   int st = 0;
   uint32_t i = 0;
   // one step reading window `use`, loading the window two steps ahead into
   // `use`.  Both steps of an iteration run on every lane (no branch between
   // them, so the loop entry keeps one memory-op order): a lane that finished
-  // in the first keeps its status and stores its second record into the
-  // block's spare slot.
-  auto step = [&](Win6& use, bool live) -> bool {
+  // in the first keeps its status and leaves the pair it stored alone.
+  auto step = [&](Win6& use, bool live, bool even) -> bool {
     uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
     if (K3_SYM) {
       eLL = k3_entry(eLL, 0);
@@ -988,14 +1004,20 @@ __device__ int seq_chain2(const uint8_t* bs, uint32_t bs_size, uintptr_t base, T
     sLL = (nsL << nbL) + vL - TL;
     sML = (nsM << nbM) + vM - TM;
     sOF = (nsO << nbO) + vO - TO;
+    const uint32_t stw = sLL | (sML << 10) | (sOF << 20);   // record i + 1
     asm volatile("" ::: "memory");
-    k3_store(out + (live ? i + 1 : n), (uint32_t)pos, sLL | (sML << 10) | (sOF << 20));
+    if (even) {
+      k3_store_pair(out + i, pPos, pSt, (uint32_t)pos, stw);
+    } else {
+      pPos = (uint32_t)pos;
+      pSt = stw;
+    }
     i++;
     return !live || sst != 0 || last;
   };
   for (;;) {
-    const bool d1 = step(wa, true);
-    const bool d2 = step(wb, !d1);
+    const bool d1 = step(wa, true, true);
+    const bool d2 = step(wb, !d1, false);
     if (d2) break;
   }
   return st;
@@ -1099,27 +1121,25 @@ __device__ int seq_chainfl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, 
   pos -= A;
   const uint32_t aL = all - 31, aM = alm - 31, aO = alo - 31;
   const uint32_t TL = 1u << all, TM = 1u << alm, TO = 1u << alo;
-  typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(8)));
-  const uint64_t r0 = (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
-  // loop entry: the trip's memory-op order (window, window, store, ...)
+  // record 0, then the pairs: an even step stores (record i, record i + 1),
+  // an odd step keeps its record for the next pair.  Loop entry: the trip's
+  // memory-op order (window, store, window, window, store, ...)
+  uint32_t pPos = (uint32_t)pos, pSt = sLL | (sML << 10) | (sOF << 20);
+  const uint32_t n_even = (n + 1) & ~1u;              // the spare pair
   WinN<N> w[L];
 #pragma unroll
   for (int k = 0; k < L; k++) {
     w[k] = winn_load<N>(bs, m, k == 0 ? pos0 : pos);
-    if (k & 1) {
+    if (!(k & 1)) {
       asm volatile("" ::: "memory");
-      *(u64x2u*)out = u64x2u{r0, r0};
+      k3_store_pair(out, pPos, pSt, pPos, pSt);
     }
-  }
-  if (L & 1) {
-    asm volatile("" ::: "memory");
-    *(u64x2u*)out = u64x2u{r0, r0};
   }
   uint32_t mx = 0;
   int32_t ymin = 0;
   // (forming the next LDS addresses as (ns << nb + 1) + const + 2 v, one add
   // nearer the state bits, measured slower: 14.9 vs 13.8 ms)
-  auto step = [&](WinN<N>& use) -> uint64_t {
+  auto step = [&](WinN<N>& use) -> uint32_t {
     const uint32_t eLL = tll[sLL], eOF = tof[sOF], eML = tml[sML];
     mx = max(mx, max(eLL, max(eML, eOF)));
     const uint32_t nsL = eLL & 1023, nsM = eML & 1023, nsO = eOF & 1023;
@@ -1134,19 +1154,23 @@ __device__ int seq_chainfl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, 
     sLL = (nsL << nbL) + vL - TL;
     sML = (nsM << nbM) + vM - TM;
     sOF = (nsO << nbO) + vO - TO;
-    return (uint64_t)(uint32_t)pos | ((uint64_t)(sLL | (sML << 10) | (sOF << 20)) << 32);
+    return sLL | (sML << 10) | (sOF << 20);
   };
-  for (uint32_t i = 0; i + 1 < n; i += U) {
+  uint32_t i = 0;
+  for (; i + 1 < n; i += U) {
 #pragma unroll
     for (int k = 0; k < U; k += 2) {
-      const uint64_t qa = step(w[k % L]);
-      const uint64_t qb = step(w[(k + 1) % L]);
+      const uint32_t sa = step(w[k % L]);
       asm volatile("" ::: "memory");
-      const uint32_t slot = i + 1 + k;
-      *(u64x2u*)(out + (slot < n ? slot : n)) = u64x2u{qa, qb};
+      const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
+      k3_store_pair(out + (slot < n ? slot : n_even), pPos, pSt, (uint32_t)pos, sa);
+      pSt = step(w[(k + 1) % L]);
+      pPos = (uint32_t)pos;
     }
   }
-  const uint64_t rl = *(volatile uint64_t*)(out + n - 1);
+  // the record the last trip kept (record i): the block's last when n - 1 == i
+  k3_store_pair(out + (i < n ? i : n_even), pPos, pSt, pPos, pSt);
+  const uint64_t rl = k3_reread(out, n - 1);
   const int32_t pl = (int32_t)(uint32_t)rl;
   const uint32_t st = (uint32_t)(rl >> 32);
   const uint32_t eLL = tll[st & 1023], eML = tml[(st >> 10) & 1023], eOF = tof[(st >> 20) & 1023];
@@ -1246,8 +1270,6 @@ __device__ inline uint32_t qdpp(uint32_t x) {
 }
 constexpr int QP_SWAP1 = 0xB1;   // quad_perm [1,0,3,2]
 constexpr int QP_SWAP2 = 0x4E;   // quad_perm [2,3,0,1]
-constexpr int QP_SHR1 = 0x90;    // quad_perm [0,0,1,2]
-constexpr int QP_L1TO2 = 0x10;   // quad_perm [0,0,1,0]
 __device__ inline uint32_t quad_sum(uint32_t x) {
   x += qdpp<QP_SWAP1>(x);
   return x + qdpp<QP_SWAP2>(x);
@@ -1260,12 +1282,6 @@ __device__ inline uint32_t quad_max(uint32_t x) {
   x = max(x, qdpp<QP_SWAP1>(x));
   return max(x, qdpp<QP_SWAP2>(x));
 }
-// exclusive prefix over roles 0, 1, 2 (m0: 0 in role 0, else all ones)
-__device__ inline uint32_t quad_excl(uint32_t x, uint32_t m0) {
-  const uint32_t t = qdpp<QP_SHR1>(x) & m0;
-  return t + qdpp<QP_L1TO2>(t);
-}
-
 template <int L, int N>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
@@ -1281,36 +1297,43 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   const int32_t pos0 = pos;
   const Win6 wi = win6_load(bs, m, pos);
   const uint32_t v0 = win6_bits(wi, pos, (uint32_t)A);
-  // this lane's role: OF (0) | ML (1) | LL (2) | LL's shadow (3, masked by m3)
+  // this lane's role: OF (0) | ML (1) | LL (2) | LL's shadow (3: the LL
+  // table and the LL lane's bit offsets, so it tracks the LL state exactly;
+  // masked out of the count sums by m3)
   const int alr = role == 0 ? alo : role == 1 ? alm : all;
   const uint32_t m3 = role == 3 ? 0u : ~0u, m0 = role == 0 ? 0u : ~0u;
   const uint32_t ar = (uint32_t)(alr - 31), Tr = 1u << alr;
-  const uint32_t shr = role == 0 ? 20 : role == 1 ? 10 : 0;
   uint32_t s = role == 0 ? __builtin_amdgcn_ubfe(v0, alm, alo)
              : role == 1 ? __builtin_amdgcn_ubfe(v0, 0, alm)
              : v0 >> (alo + alm);
   pos -= A;
-  typedef uint64_t u64x2u __attribute__((ext_vector_type(2), aligned(8)));
-  const uint64_t r0 = (uint64_t)(uint32_t)pos | ((uint64_t)quad_or((s << shr) & m3) << 32);
-  const bool writer = role == 0;
+  // Records in pairs (zd_common.h), one dword per lane and no cross-lane
+  // moves: OF lane x (its two states and the position step), ML lane y, LL
+  // lane z, shadow w (the pair's first position).  An even step stores the
+  // pair (record i, record i + 1), an odd one keeps its record.
+  uint32_t pS = s, pPos = (uint32_t)pos;
+  auto pair_word = [&](uint32_t sB, uint32_t posB) -> uint32_t {
+    const uint32_t d = pS | (sB << 10);
+    const uint32_t x = d | ((pPos - posB) << 20);
+    return role == 3 ? pPos : (role == 0 ? x : d);
+  };
+  g_u32* const outw = (g_u32*)out + role;
+  const uint32_t n_even = (n + 1) & ~1u;              // the spare pair
+  // loop entry: the trip's memory-op order (window, store, window, window, store, ...)
   WinN<N> w[L];
 #pragma unroll
   for (int k = 0; k < L; k++) {
     w[k] = winn_load<N>(bs, m, k == 0 ? pos0 : pos);
-    if (k & 1) {
+    if (!(k & 1)) {
       asm volatile("" ::: "memory");
-      if (writer) *(u64x2u*)out = u64x2u{r0, r0};
+      outw[0] = pair_word(s, (uint32_t)pos);
     }
-  }
-  if (L & 1) {
-    asm volatile("" ::: "memory");
-    if (writer) *(u64x2u*)out = u64x2u{r0, r0};
   }
   uint32_t mx = 0;
   int32_t ymin = 0;
-  auto step = [&](WinN<N>& use) -> uint64_t {
+  auto step = [&](WinN<N>& use) {
     const uint32_t e = tab[s];
-    mx = max(mx, e & m3);
+    mx = max(mx, e);                                // (the shadow lane's e is the LL lane's)
     const uint32_t ns = e & 1023, nb = __builtin_clz(ns) + ar;
     // the three roles' counts by three quad broadcasts and one add3 (the
     // shadow lane's count never enters), y from the position before the step
@@ -1322,23 +1345,31 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     ymin = min(ymin, y);
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
     use = winn_load<N>(bs, m, pos);
-    const uint32_t v = __builtin_amdgcn_ubfe(r, quad_excl(nb, m0), nb);
+    // the state bits sit OF | ML | LL upwards from y: offsets 0, nbO, nbO +
+    // nbM (the shadow takes the LL lane's), by quad_perm [0,0,1,1] twice
+    const uint32_t t = qdpp<0x50>(nb) & m0;
+    const uint32_t v = __builtin_amdgcn_ubfe(r, t + qdpp<0x50>(t), nb);
     s = (ns << nb) + v - Tr;   // (the next address formed from v in one op: 2.07 -> 2.11 ms on C3)
-    return (uint64_t)(uint32_t)pos | ((uint64_t)quad_or((s << shr) & m3) << 32);
   };
-  for (uint32_t i = 0; i + 1 < n; i += U) {
+  uint32_t i = 0;
+  for (; i + 1 < n; i += U) {
 #pragma unroll
     for (int k = 0; k < U; k += 2) {
-      const uint64_t qa = step(w[k % L]);
-      const uint64_t qb = step(w[(k + 1) % L]);
+      step(w[k % L]);
       asm volatile("" ::: "memory");
-      const uint32_t slot = i + 1 + k;
-      if (writer) *(u64x2u*)(out + (slot < n ? slot : n)) = u64x2u{qa, qb};
+      const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
+      outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
+      step(w[(k + 1) % L]);
+      pS = s;
+      pPos = (uint32_t)pos;
     }
   }
-  const uint64_t rl = *(volatile uint64_t*)(out + n - 1);
+  // the record the last trip kept (record i): the block's last when n - 1 == i
+  outw[2 * (i < n ? i : n_even)] = pair_word(pS, pPos);
+  const uint64_t rl = k3_reread(out, n - 1);
   const int32_t pl = (int32_t)(uint32_t)rl;
   const uint32_t st = (uint32_t)(rl >> 32);
+  const uint32_t shr = role == 0 ? 20 : role == 1 ? 10 : 0;
   const uint32_t el = tab[(st >> shr) & 1023] & m3;
   mx = quad_max(max(mx, el));
   const uint32_t S = quad_sum((__builtin_clz(el & 1023) + ar) & m3);
@@ -1418,6 +1449,16 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
                                  al[1], al[2], C.nseq, recs + C.seq_out);
   if (st) k3_fail(C, ci, cstate, fstate, st);
 }
+// A K3 record pair read as 8-byte halves, record i's slot on lane i (a batch
+// starting at an even record): the halves are exchanged with the partner lane
+// and the lane's record unpacked (zd_common.h).  All 64 lanes active.
+__device__ inline uint64_t rec_lane(uint64_t raw, int lane) {
+  const uint32_t lo = (uint32_t)raw, hi = (uint32_t)(raw >> 32);
+  const uint32_t plo = qdpp<QP_SWAP1>(lo), phi = qdpp<QP_SWAP1>(hi);
+  const uint32_t h = lane & 1;
+  return rec_unpack(h ? plo : lo, h ? phi : hi, h ? lo : plo, h ? hi : phi, h);
+}
+
 // ---------------------------------------------------------------------------
 // K4: execute (decoding_context.rs:50-106 + block.rs:74-99), one frame per
 // wave, one sequence per lane, 64 sequences per batch.  A frame that decodes
@@ -1803,7 +1844,15 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     // for the window's room leaves the batch loop; the whole wave copies it
     // and the pipeline restarts after it.
     const bool lit_stage = lsrc != nullptr;
-    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n ? SQ[i] : 0; };
+    // K3 records come in pairs (zd_common.h), a block's first at an even
+    // index: lane i loads record i's 8-byte slot, half of its pair, and the
+    // halves are exchanged with the partner lane once the load has landed
+    // (rec_lane, at the wait that is there anyway).  A pipeline restart at an
+    // odd record runs that one sequence alone, so batches start even.  The
+    // context API's direct records are one 8-byte word each.
+    const uint32_t n_ld = direct ? n : (n + 1) & ~1u;
+    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n_ld ? SQ[i] : 0; };
+    auto rec_of = [&](uint64_t raw) -> uint64_t { return direct ? raw : rec_lane(raw, lane); };
     auto win_of = [&](uint64_t r, bool v) -> WinU {
       return winu_load(bsp, (uintptr_t)src, (v && !direct) ? (int32_t)(uint32_t)r : 0);
     };
@@ -1811,15 +1860,18 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
       return (lit_stage && 16 * (uint32_t)lane < K4_STG && cur + 16 * (uint32_t)lane < nl) ? ldg16_once(lsrc + cur + 16 * lane) : f4;
     };
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
-      uint64_t recA = rec_at(s0 + lane), recB = rec_at(s0 + 64 + lane);
-      WinU winA = win_of(recA, s0 + lane < n);
+      const bool odd0 = !direct && (s0 & 1);        // a restart at an odd record
+      const uint32_t vlim = odd0 ? s0 + 1 : n;       // (that record alone)
+      uint64_t recA = odd0 ? (lane == 0 ? rec_get(SQ, s0, false) : 0) : rec_of(rec_at(s0 + lane));
+      uint64_t recB = rec_at(s0 + 64 + lane);
+      WinU winA = win_of(recA, s0 + lane < vlim);
       u32x4 litA = lit_of(lit_cursor);
       bool big = false;                              // batch loop left for one large sequence
       uint32_t bll = 0, bml = 0;
       uint64_t boff = 0;
       for (;;) {
         const uint32_t i = s0 + lane;
-        const bool valid = i < n;
+        const bool valid = i < vlim;
         K4_PHASE(7);
         // this batch's literal bytes from the cursor on; lanes past the stage
         // all store into its 16-byte tail (only ever read as overshoot):
@@ -1832,7 +1884,8 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         wait_vm();
         fl_safe = X.fl;
         // the next batch's windows and the records after it, first thing
-        const WinU winB = win_of(recB, s0 + 64 + lane < n);
+        const uint64_t recBv = rec_of(recB);
+        const WinU winB = win_of(recBv, s0 + 64 + lane < n);
         const uint64_t recC = rec_at(s0 + 128 + lane);
         k4_flush(X, false);
         // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
@@ -2047,7 +2100,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         s0 += k;
         K4_PHASE(5);
         if (k < 64 || s0 >= n) break;                  // a partial batch: the pipeline restarts at s0
-        recA = recB; winA = winB; recB = recC; litA = litB;
+        recA = recBv; winA = winB; recB = recC; litA = litB;
       }
       k4_flush(X, false);                            // k4_room and the large-sequence path expect it
       if (big && err_key == KEY_NONE) {
@@ -2277,7 +2330,7 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
       for (int k = 0; k < K4F_KC; k++) {
         ll[k] = 0; ml[k] = 0; oc[k] = 4;          // padding: no bytes, a fresh offset
         if (b0 + k < cn) {
-          const uint64_t sq = SQ[c0 + b0 + k];
+          const uint64_t sq = rec_get(SQ, c0 + b0 + k, direct);
           if (direct) {
             ll[k] = seq_ll(sq); ml[k] = seq_ml(sq); oc[k] = seq_off(sq);
           } else {
@@ -2693,9 +2746,16 @@ struct JRecs {
   const uint8_t* bsp;
   uintptr_t base;
   uint32_t n;
+  bool direct;
   uint64_t recA, recB;
   WinU winA;
-  __device__ inline uint64_t at(uint32_t i) const { return i < n ? SQ[i] : 0; }
+  // record i (K3's pairs, zd_common.h, or a direct word)
+  __device__ inline uint64_t at(uint32_t i) const {
+    if (i >= n) return 0;
+    if (direct) return SQ[i];
+    const u32x4g v = *(const g_u32x4g*)(SQ + (i & ~1u));
+    return rec_unpack(v.x, v.y, v.z, v.w, i & 1);
+  }
   __device__ inline WinU win(uint64_t r, bool v) const { return winu_load(bsp, base, v ? (int32_t)(uint32_t)r : 0); }
   __device__ inline void start(uint32_t s0, int lane) {
     recA = at(s0 + lane);
@@ -2744,7 +2804,7 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
       const uint32_t n = C.nseq;
       if (n) {
         j_stab(stab, C, comp, cstate, fses, lane);
-        JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n};
+        JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n, C.seq_direct != 0};
         R.start(0, lane);
         for (uint32_t s0 = 0; s0 < n; s0 += 64) {
           if (s0 && s0 % J_SEG == 0 && lane == 0) {  // a checkpoint for KJ3's segment
@@ -2930,7 +2990,7 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
   const uint32_t sb = SD.k * J_SEG, se = min(n, sb + J_SEG);
   if (se > sb) {
     j_stab(stab, C, comp, cstate, fses, lane);
-    JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, se};
+    JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, se, C.seq_direct != 0};
     R.start(sb, lane);
     for (uint32_t s0 = sb; s0 < se; s0 += 64) {
       const int k = (int)min(64u, se - s0);
