@@ -134,6 +134,12 @@ constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 3 * 256;
 // compressed block) / off.
 constexpr uint32_t K4J_MIN_BLOCKS = 16;
 constexpr size_t K4J_MAX_FRAMES = 1024;
+// A plan of few frames leaves the GPU nearly idle with one wave per frame on
+// the streaming K4 (the reference's moby-dick sample: one frame of 10 blocks,
+// 159k sequences on one wave): there K4J takes every frame of 2 or more
+// compressed blocks.
+constexpr size_t K4J_FEW_FRAMES = 64;
+constexpr uint32_t K4J_MIN_BLOCKS_FEW = 2;
 constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
 constexpr size_t FRAMES_INDEX_SERIAL_MAX = 4096;     // zd_frames_index asked for at most this many frames: walk only them
 
@@ -161,6 +167,7 @@ struct PlanCtx {
   uint32_t flags;
   bool k4f_on, k4j_auto;
   int k4j_mode;
+  uint32_t k4j_min;        // compressed blocks a frame needs for K4J (automatic mode)
 };
 
 // Where the filling pass writes: the plan's host vectors (small plans, the
@@ -294,7 +301,7 @@ void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks,
   // K4J: frames of many compressed blocks (u32 positions)
   const bool to_j = X.out_len0 == 0 && !frame_failed_host && fd.nblocks && hf.ncomp && hf.d.kind == ZD_FRAME_ZSTD &&
                     cap <= K4J_MAX_FRAME_OUT &&
-                    (X.k4j_mode >= 0 ? X.k4j_mode == 1 : (X.k4j_auto && hf.ncomp >= K4J_MIN_BLOCKS));
+                    (X.k4j_mode >= 0 ? X.k4j_mode == 1 : (X.k4j_auto && hf.ncomp >= X.k4j_min));
   // the streaming K4 keeps int32 frame positions: larger frames with
   // sequences that K4J does not take are outside the GPU path's domain
   if (!to_j && cap > K4_MAX_FRAME_OUT && seqs_in_frame)
@@ -458,10 +465,11 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   X.k4f_on = k4f_env ? atoi(k4f_env) == 1 : P->nframes >= K4F_AUTO_MIN_FRAMES && P->nframes <= K4F_AUTO_MAX_FRAMES;
   static const char* k4j_env = getenv("ZD_K4J");
   X.k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0 : (k4j_env ? atoi(k4j_env) : -1);
+  X.k4j_min = P->nframes <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
   size_t j_candidates = 0;
   if (X.k4j_mode < 0 && out_len0 == 0)
     for (const HostPart& hp : P->parts)
-      for (const HostFrame& hf : hp.frames) j_candidates += hf.key == KEY_NONE && hf.ncomp >= K4J_MIN_BLOCKS;
+      for (const HostFrame& hf : hp.frames) j_candidates += hf.key == KEY_NONE && hf.ncomp >= X.k4j_min;
   X.k4j_auto = j_candidates > 0 && j_candidates <= K4J_MAX_FRAMES;
 
   const size_t np = P->parts.size();
