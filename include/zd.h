@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 5
+#define ZD_ABI_VERSION 6
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -171,6 +171,12 @@ typedef struct zd_plan_info {
   uint64_t io_h2d_ns;      /* the last zd_plan_decompress: input host -> HBM */
   uint64_t io_decode_ns;   /*   decode + results (kernels, status read-back) */
   uint64_t io_d2h_ns;      /*   output HBM -> host */
+  uint64_t error_key;      /* the last zd_plan_results: where the first failing frame stopped,
+                              phase << 62 | block in frame << 32 | stage << 28 | sub << 8 | -status
+                              (phase 0 parse, 1 decode, 3 a limit of the GPU path; stages
+                              csrc/zd_common.h); all ones when every frame decoded */
+  uint64_t replans;        /* the last zd_plan_decompress: re-plans past frames that overran
+                              their reserved capacity (or K4J rounds), 0 normally */
 } zd_plan_info;
 
 /* Index src[0..n) on the host and allocate the plan's device workspace.

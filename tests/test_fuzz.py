@@ -3,9 +3,9 @@ target (zstd-decompressor/fuzz/fuzz_targets/fuzz_target_1.rs: iterate the
 frames of arbitrary bytes, decode each, never crash).  Seeded structure-aware
 mutations of valid frames (header fields, block headers, literal/sequence
 section headers, splices, truncations, random tails) go through the GPU path;
-every input must come back with the oracle's status and bytes (or, for inputs
-that decode past their declared size, ZD_E_OUT_OF_DOMAIN), and the process must
-survive all of them."""
+every input must come back with the oracle's status and bytes, and the process
+must survive all of them.  ZD_E_OUT_OF_DOMAIN (a limit of the GPU path,
+DESIGN.md) fails a campaign; ZD_FUZZ_DUMP=DIR keeps such inputs."""
 import os
 import random
 
@@ -78,7 +78,7 @@ def test_fuzz_structure_aware():
         assert gout == oout, f"#{it}: output differs"
         seen["ok" if ost == 0 else "err"] += 1
     print("fuzz outcome counts:", seen)
-    assert seen["ood"] <= max(30, iters // 10), seen
+    assert seen["ood"] == 0, seen
 
 
 def test_fuzz_forked_plans():
@@ -110,12 +110,22 @@ def test_fuzz_forked_plans():
         assert gout == oout, f"#{it}: output differs"
         seen["ok" if ost == 0 else "err"] += 1
     print("fuzz outcome counts (plans):", seen)
-    assert seen["ood"] <= max(8, iters // 10), seen
+    assert seen["ood"] == 0, seen
 
 
 # (seed, input index) of campaign inputs that once disagreed with the oracle
 REGRESSIONS = [
-    (6, 4281),   # runaway Huffman-weight stream before a reserved sequence-mode bit: oracle REF_PANIC
+    (6, 4281),     # runaway Huffman-weight stream before a reserved sequence-mode bit: oracle REF_PANIC
+    # (seed 601: inputs that left the GPU path's domain before round 3)
+    (601, 1103),   # Huffman tree of maxBits > 12, an absent node reached: REF_PANIC (deep_build)
+    (601, 1140),
+    (601, 2459),
+    (601, 36),     # streams decode 53 literals past Regenerated_Size: re-planned with room
+    (601, 1046),
+    (601, 1307),   # back-to-back streams end within 16 bytes past R (K2's slack now past them)
+    (601, 1531),   # frame decodes past its Frame_Content_Size: re-planned with 4x capacity
+    (601, 2835),
+    (601, 2183),
 ]
 
 
@@ -129,7 +139,5 @@ def test_fuzz_regressions():
             p = r.random() < 0.3
         ost, oout = oracle.decompress_status(data, p)
         gst, gout = decompress_status(data, p)
-        if gst == OUT_OF_DOMAIN:
-            continue
         assert gst == ost, f"seed {seed} #{idx}: oracle {ost}, gpu {gst}"
         assert gout == oout, f"seed {seed} #{idx}: output differs"

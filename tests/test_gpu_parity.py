@@ -2,8 +2,9 @@
 restatement of the reference decoder — on the same inputs.
 
 Bit-exact output is required wherever the oracle succeeds; wherever it fails
-the GPU path must fail too, with the same reference error variant (a frame the
-GPU path cannot reproduce reports ZD_E_OUT_OF_DOMAIN, counted separately).
+the GPU path must fail too, with the same reference error variant.  A frame
+past the GPU path's limits would report ZD_E_OUT_OF_DOMAIN: no
+input here may.
 """
 import random
 
@@ -15,7 +16,7 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-REF_PANIC, OUT_OF_DOMAIN = -90, -91
+OUT_OF_DOMAIN = -91
 
 
 def gpu(data, p=False, flags=0):
@@ -23,21 +24,18 @@ def gpu(data, p=False, flags=0):
     return decompress_status(data, p, flags)
 
 
-def assert_parity(data, p=False, what="", allow_ood=False, flags=0):
-    """allow_ood: the input may leave the GPU path's domain (corrupted input
-    decoding past its declared content size)."""
+def assert_parity(data, p=False, what="", flags=0):
+    """Status and output as the oracle's; ZD_E_OUT_OF_DOMAIN (a limit of the
+    GPU path) fails the test."""
     ost, oout = oracle.decompress_status(data, p)
     gst, gout = gpu(data, p, flags)
-    if allow_ood and gst == OUT_OF_DOMAIN:
-        return ost, gst
+    assert gst != OUT_OF_DOMAIN, f"{what}: out of the GPU path's domain (oracle status {ost})"
     if ost == 0:
         assert gst == 0, f"{what}: oracle ok, gpu status {gst}"
         assert gout == oout, f"{what}: output differs (len {len(gout)} vs {len(oout)})"
     else:
-        assert gst != 0, f"{what}: oracle status {ost}, gpu ok"
-        if gst != OUT_OF_DOMAIN:
-            assert gst == ost, f"{what}: oracle status {ost}, gpu status {gst}"
-            assert gout == oout, f"{what}: partial output of the frames before the failure differs"
+        assert gst == ost, f"{what}: oracle status {ost}, gpu status {gst}"
+        assert gout == oout, f"{what}: partial output of the frames before the failure differs"
     return ost, gst
 
 
@@ -160,16 +158,16 @@ def test_corrupted_inputs():
     r = random.Random(1234)
     src = gen.text(200_000, seed=11)
     base = gen.frames(src, 64 << 10, 3) + gen.frames(gen.binary(100_000), 50_000, 9)
-    stats = {"ok": 0, "err_same": 0, "ood": 0}
+    stats = {"ok": 0, "err_same": 0}
     for it in range(300):
         d = bytearray(base)
         for _ in range(r.randrange(1, 4)):
             d[r.randrange(len(d))] = r.randrange(256)
         if r.random() < 0.2:
             d = d[: r.randrange(len(d))]
-        ost, gst = assert_parity(bytes(d), False, f"corrupt #{it}", allow_ood=True)
-        stats["ok" if ost == 0 else ("ood" if gst == OUT_OF_DOMAIN else "err_same")] += 1
-    assert stats["ok"] + stats["err_same"] >= 290, stats
+        ost, gst = assert_parity(bytes(d), False, f"corrupt #{it}")
+        stats["ok" if ost == 0 else "err_same"] += 1
+    assert stats["ok"] and stats["err_same"], stats
 
 
 def test_corrupted_inputs_forked_plan():
@@ -185,15 +183,15 @@ def test_corrupted_inputs_forked_plan():
     spans = [(f["src_offset"], f["src_size"]) for f in frames_index(base)[0]]
     assert len(spans) == 300
     assert_parity(base, False, "forked plan, intact")
-    stats = {"ok": 0, "err_same": 0, "ood": 0}
+    stats = {"ok": 0, "err_same": 0}
     for it in range(60):
         d = bytearray(base)
         o, n = spans[r.randrange(20, 280)]
         for _ in range(r.randrange(1, 4)):
             d[o + r.randrange(n)] = r.randrange(256)
-        ost, gst = assert_parity(bytes(d), False, f"forked corrupt #{it}", allow_ood=True)
-        stats["ok" if ost == 0 else ("ood" if gst == OUT_OF_DOMAIN else "err_same")] += 1
-    assert stats["ok"] + stats["err_same"] >= 55, stats
+        ost, gst = assert_parity(bytes(d), False, f"forked corrupt #{it}")
+        stats["ok" if ost == 0 else "err_same"] += 1
+    assert stats["ok"] and stats["err_same"], stats
 
 
 def test_multi_block_frames_forked_plan():
@@ -217,7 +215,7 @@ def test_multi_block_frames_forked_plan():
         f = frames[r.randrange(4, 32)]
         for _ in range(r.randrange(1, 3)):
             d[f["src_offset"] + r.randrange(f["src_size"])] = r.randrange(256)
-        assert_parity(bytes(d), False, f"multi-block forked corrupt #{it}", allow_ood=True)
+        assert_parity(bytes(d), False, f"multi-block forked corrupt #{it}")
 
 
 def test_parallel_host_walk():
@@ -244,7 +242,7 @@ def test_parallel_host_walk():
             d[f["src_offset"] + r.randrange(f["src_size"])] = r.randrange(256)
         if it % 8 == 7:
             d = d[: f["src_offset"] + r.randrange(f["src_size"])]
-        assert_parity(bytes(d), False, f"parallel walk corrupt #{it} (frame {k})", allow_ood=True)
+        assert_parity(bytes(d), False, f"parallel walk corrupt #{it} (frame {k})")
 
 
 def test_many_frame_roundtrip_large():
@@ -275,7 +273,7 @@ def test_one_lane_k3_chain(resources):
             d = bytearray(base)
             for _ in range(r.randrange(1, 4)):
                 d[r.randrange(len(d))] = r.randrange(256)
-            assert_parity(bytes(d), False, f"flags={flags} corrupt #{it}", allow_ood=True, flags=flags)
+            assert_parity(bytes(d), False, f"flags={flags} corrupt #{it}", flags=flags)
 
 
 def test_plan_decompress_reuses_the_plan(resources):
@@ -315,7 +313,7 @@ def test_one_round_plan():
         o, n = spans[r.randrange(100, 2900)]
         for _ in range(r.randrange(1, 4)):
             d[o + r.randrange(n)] = r.randrange(256)
-        assert_parity(bytes(d), False, f"per-CU plan corrupt #{it}", allow_ood=True)
+        assert_parity(bytes(d), False, f"per-CU plan corrupt #{it}")
 
 
 def _ncount(al, probs):
@@ -375,16 +373,18 @@ def test_k1_large_tables():
             content = lits + seqs
             hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
             frame = b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x00]) + hdr + content
-            assert_parity(frame, False, f"nsym {nsym} al {al} trial {trial}", allow_ood=True)
+            assert_parity(frame, False, f"nsym {nsym} al {al} trial {trial}")
 
 
-def _deep_tree_frame(r, nbytes):
-    """One frame, one compressed block: a Huffman tree of maxBits 12 (direct
-    weights 12, 11, ..., 1 and the implied last symbol) over a random literal
-    bitstream (every bit pattern decodes: the tree is complete), then one
-    sequence from random bits with the predefined tables."""
-    weights = list(range(12, 0, -1))                       # symbols 0..11; symbol 12 implied
-    desc = bytes([127 + len(weights)]) + bytes((weights[i] << 4) | weights[i + 1] for i in range(0, 12, 2))
+def _deep_tree_frame(r, nbytes, weights=None):
+    """One frame, one compressed block: a Huffman tree of direct weights
+    (default maxBits 12: weights 12, 11, ..., 1 and the implied last symbol,
+    a complete tree: every bit pattern decodes) over a random literal
+    bitstream, then one sequence from random bits with the predefined tables."""
+    if weights is None:
+        weights = list(range(12, 0, -1))                   # symbols 0..11; symbol 12 implied
+    w = list(weights) + [0] * (len(weights) & 1)
+    desc = bytes([127 + len(weights)]) + bytes((w[i] << 4) | w[i + 1] for i in range(0, len(w), 2))
     stream = bytes(r.randrange(256) for _ in range(nbytes - 1)) + bytes([r.randrange(1, 256)])
     comp = len(desc) + len(stream)
     regen = 1023                                            # >= what the stream decodes (the reference ignores it, D8)
@@ -412,6 +412,39 @@ def test_k2_deep_trees_beside_libzstd_frames():
     assert ost == 0
     for i, f in enumerate(deep_err[:8]):
         assert_parity(f, False, f"deep tree, rejected #{i}")
+
+
+def test_k2_trees_deeper_than_the_lut():
+    """Trees of maxBits 13..21 (non-conforming: zstd stops at 11) have no LUT;
+    K1 keeps their codes as intervals and K2 decodes them symbol by symbol
+    (zd_kernels.hip deep_build / huf_stream_deep).  Complete trees (weights
+    p..1) and random weights (absent tree nodes at any depth: the reference
+    panics there, or runs out of bits first), alone and inside a plan of
+    libzstd frames; streams that decode past Regenerated_Size re-plan their
+    frame with room for the literals (zd_plan_decompress)."""
+    r = random.Random(23)
+    ok, frames = [], []
+    for p in range(13, 16):                 # complete trees: a frame of each depth the reference decodes
+        for _ in range(100):
+            f = _deep_tree_frame(r, r.randrange(20, 300), list(range(p, 0, -1)))
+            frames.append(f)
+            if oracle.decompress_status(f, False)[0] == 0:
+                ok.append(f)
+                break
+    assert len(ok) == 3
+    for _ in range(40):
+        n = r.randrange(2, 128)
+        weights = [r.choice([0, 0, r.randrange(1, 16)]) for _ in range(n)]
+        weights[r.randrange(n)] = r.randrange(12, 16)
+        frames.append(_deep_tree_frame(r, r.randrange(20, 300), weights))
+    for i, f in enumerate(frames):
+        assert_parity(f, False, f"deep tree #{i}")
+    src = gen.text(200_000, seed=5)
+    parts = []
+    for i in range(9):
+        parts.append(ok[i // 3] if i % 3 == 1 else gen.frames(src[i * 12_000:(i + 1) * 12_000], 12_000, 3))
+    ost, _ = assert_parity(b"".join(parts), False, "deep trees inside libzstd frames")
+    assert ost == 0
 
 
 @pytest.mark.parametrize("shape", ["one_frame", "forked_300_frames", "block_parallel"])

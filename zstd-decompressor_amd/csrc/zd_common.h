@@ -292,6 +292,14 @@ enum : uint32_t { PH_PARSE = 0, PH_DECODE = 1, PH_LIMIT = 3 };
 enum : uint32_t { PS_STRUCT = 0, PS_HUF_DESC = 1, PS_JUMP = 2, PS_SEQ_HDR = 3, PS_SEQ_TABLES = 4, PS_ALL = 5 };
 // decode stages inside Block::decode (block.rs:80-87)
 enum : uint32_t { DS_LITERALS = 1, DS_SEQUENCES = 2, DS_EXECUTE = 3 };
+// PH_LIMIT stages the host can act on: a frame that decodes past the capacity
+// its plan reserved (re-planned with more, zd_plan_decompress), K4J's
+// pointer jumping not converging within its rounds (re-planned streaming)
+enum : uint32_t { LS_CAPACITY = 7, LS_JROUNDS = 8 };
+// sub of the DS_LITERALS out-of-domain key of a block whose streams decoded
+// more literals than its slot holds (re-planned with room, zd_plan_decompress)
+constexpr uint32_t DS_LIT_OVERFLOW_SUB = 4;
+ZD_HD inline uint32_t key_stage(uint64_t k) { return (uint32_t)((k >> 28) & 15); }
 
 ZD_HD inline uint64_t make_key(uint32_t phase, uint32_t block, uint32_t stage, uint32_t sub, int code) {
   return ((uint64_t)(phase & 3) << 62) | ((uint64_t)(block & 0x3FFFFFFFu) << 32) |
@@ -323,6 +331,8 @@ struct CompBlock {
   uint32_t seq_tables;     // rel: first byte after nbSeq + mode byte
   uint32_t lut_slot;       // Huffman LUT slot this block builds (LIT_COMPRESSED)
   uint32_t fse_slot;       // FSE slot this block builds (nseq > 0)
+  uint32_t lit_extra;      // literal slot bytes past Regenerated_Size + 16: a re-planned frame's blocks get
+                           // room for all their streams decode (8 per stream byte), zd_plan_decompress
   int32_t huf_src;         // comp index whose LUT the literals use (-1: none)
   int32_t tab_src[3];      // comp index whose LL/OF/ML table the sequences use (-1: none)
   uint8_t lit_type;
@@ -437,6 +447,7 @@ struct Workspace {
   uint64_t lits, seqs, luts, fses;
   uint64_t jframes, jblkd, jblk, jseg, jsegd, jpend;    // K4J descriptors / state / round counters
   uint64_t jdone;                                       // K4J: one byte per piece, 1 once emitted
+  uint64_t huge;                                        // K1: u32 count + the blocks whose trees have > 256 symbols
   uint64_t jst;                                         // K4J per-byte state words
   uint64_t total;
 };

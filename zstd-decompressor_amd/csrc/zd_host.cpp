@@ -85,6 +85,11 @@ struct zd_plan {
   uint8_t* d_staging = nullptr;          // when the output layout is not exact
   uint64_t staging_bytes = 0;
   int index_status = 0;
+  uint64_t cap0 = 0;                     // capacity of frame 0 instead of its own (a re-plan, zd_plan_decompress)
+  // the first failing frame of the last zd_plan_results when its failure is
+  // a limit of the GPU path the host can lift (LS_CAPACITY, LS_JROUNDS)
+  int64_t limit_frame = -1;
+  uint32_t limit_stage = 0;
   size_t index_stop = 0;                 // frame index that failed to index (== nframes - 1) or nframes
   const HostFrame& frame(size_t f) const {
     const size_t k = (size_t)(std::upper_bound(part_f0.begin(), part_f0.end(), f) - part_f0.begin()) - 1;
@@ -162,7 +167,8 @@ struct PlanCounts {
 struct PlanCtx {
   int32_t prev_huf;
   int32_t prev_tab[3];
-  uint64_t out_len0, fixed_cap;
+  uint64_t out_len0, fixed_cap, cap0;
+  const HostFrame* cap0_frame;   // the plan's first frame (cap0 applies to it)
   uint64_t rep0[3];
   uint32_t flags;
   bool k4f_on, k4j_auto;
@@ -204,6 +210,9 @@ void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks,
   bool seqs_in_frame = false;
   const bool frame_failed_host = hf.key != KEY_NONE;
   uint64_t jseg = 0;
+  // a re-plan of a frame that overran (zd_plan_decompress): by identity, the
+  // counting pass numbers each part's frames from 0
+  const bool replanned = X.cap0 && &hf == X.cap0_frame && hf.d.kind == ZD_FRAME_ZSTD;
   for (uint32_t bi = 0; bi < hf.nb; bi++) {
     const HostBlock& hb = hblocks[hf.b0 + bi];
     BlockRec br{};
@@ -250,8 +259,14 @@ void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks,
       }
       // workspace
       if (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) {
+        cb.lit_extra = 0;
+        if (replanned) {             // a symbol is at least one bit: <= 8 literals per stream byte
+          uint64_t most = 0;
+          for (int k = 0; k < cb.nstreams; k++) most += 8ull * cb.stream_size[k];
+          if (most > cb.lit_regen) cb.lit_extra = (uint32_t)(most - cb.lit_regen);
+        }
         cb.lit_out = c.lits;
-        c.lits += align_up((uint64_t)cb.lit_regen + 16, 16);
+        c.lits += align_up((uint64_t)cb.lit_regen + 24 + cb.lit_extra, 16);   // + K2's 8-byte slack
       }
       cb.seq_out = c.nrec;
       c.nseq += cb.nseq;
@@ -296,6 +311,10 @@ void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks,
   }
   if (frame_failed_host) fd.nblocks = 0;
   if (X.fixed_cap) cap = X.fixed_cap;
+  if (replanned) {
+    cap = X.cap0;
+    c.exact = false;
+  }
   fd.out = c.out;
   fd.out_cap = cap;
   // K4J: frames of many compressed blocks (u32 positions)
@@ -460,6 +479,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   for (int k = 0; k < 3; k++) { X.prev_tab[k] = prev_tab[k]; X.rep0[k] = rep0[k]; }
   X.out_len0 = out_len0;
   X.fixed_cap = fixed_cap;
+  X.cap0 = P->cap0;
+  X.cap0_frame = nullptr;
+  for (const HostPart& hp : P->parts)
+    if (!hp.frames.empty()) { X.cap0_frame = hp.frames.data(); break; }
   X.flags = P->flags;
   static const char* k4f_env = getenv("ZD_K4F");
   X.k4f_on = k4f_env ? atoi(k4f_env) == 1 : P->nframes >= K4F_AUTO_MIN_FRAMES && P->nframes <= K4F_AUTO_MAX_FRAMES;
@@ -593,6 +616,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   }
 
   W.comp_state = carve(sizeof(CompState) * std::max<uint64_t>(T.comps, 1));
+  W.huge = carve(4 * (std::max<uint64_t>(T.tables, 1) + 1));
   W.frame_state = carve(sizeof(FrameState) * std::max<uint64_t>(T.frames, 1));
   W.lits = carve(T.lits + 64);
   W.seqs = carve(8 * T.nrec + 64);
@@ -1380,10 +1404,11 @@ extern "C" {
 // zd_plan_create / zd_plan_create_device: the walk (host or device), then
 // the descriptors, the workspace and the upload.
 static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint32_t flags, hipStream_t s,
-                       zd_plan** out) {
+                       zd_plan** out, uint64_t cap0) {
   zd_plan* P = new (std::nothrow) zd_plan();
   if (!P) return ZD_E_NO_MEMORY;
   P->flags = flags;
+  P->cap0 = cap0;
   const auto t0 = std::chrono::steady_clock::now();
   if (d_src) {
     if (int r = plan_index_dev(P, d_src, n, s)) { zd_plan_destroy(P); return r; }
@@ -1420,13 +1445,13 @@ static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint3
 
 int zd_plan_create(const uint8_t* src, size_t n, uint32_t flags, zd_plan** out) {
   if (!out || (!src && n)) return ZD_E_INVALID_ARG;
-  return plan_create(src, nullptr, n, flags, nullptr, out);
+  return plan_create(src, nullptr, n, flags, nullptr, out, 0);
 }
 
 int zd_plan_create_device(const uint8_t* d_src, size_t n, uint32_t flags, void* stream, zd_plan** out) {
   if (!out || (!d_src && n)) return ZD_E_INVALID_ARG;
   static const uint8_t none = 0;
-  return plan_create(nullptr, d_src ? d_src : &none, n, flags, (hipStream_t)stream, out);
+  return plan_create(nullptr, d_src ? d_src : &none, n, flags, (hipStream_t)stream, out, 0);
 }
 
 int zd_plan_info_get(const zd_plan* P, zd_plan_info* info) {
@@ -1489,6 +1514,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->d_ws + P->W.frame_state0,
                         P->n_frames * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<uint64_t>(P->n_comps, 1) * sizeof(CompState), s));
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.huge, 0, 4, s));   // K1's list of trees of more than 256 symbols
   if (P->n_jframes) {
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jdone, 0, std::max<uint64_t>(P->j_pieces, 1), s));
@@ -1543,6 +1569,9 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
   int first = -1;
   int overall = 0;
   uint64_t total = 0;
+  P->limit_frame = -1;
+  P->limit_stage = 0;
+  P->info.error_key = KEY_NONE;
   std::vector<uint64_t> from, to, len;
   bool need_compact = !P->info.out_exact;
   for (size_t f = 0; f < nf; f++) {
@@ -1551,7 +1580,22 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
     if (first >= 0) code = ZD_E_NOT_DECODED;
     if (frame_status) frame_status[f] = code;
     if (frame_len) frame_len[f] = code ? 0 : l;
-    if (code && first < 0) { first = (int)f; overall = code; }
+    if (code && first < 0) {
+      first = (int)f;
+      overall = code;
+      const uint64_t k = st[f].key;
+      P->info.error_key = k;
+      if (code == ZD_E_OUT_OF_DOMAIN && key_phase(k) == PH_LIMIT &&
+          (key_stage(k) == LS_CAPACITY || key_stage(k) == LS_JROUNDS)) {
+        P->limit_frame = (int64_t)f;
+        P->limit_stage = key_stage(k);
+      }
+      if (code == ZD_E_OUT_OF_DOMAIN && key_phase(k) == PH_DECODE && key_stage(k) == DS_LITERALS &&
+          ((k >> 8) & 0xFFFFF) == DS_LIT_OVERFLOW_SUB) {
+        P->limit_frame = (int64_t)f;
+        P->limit_stage = LS_CAPACITY;          // a re-plan gives its blocks room for every literal
+      }
+    }
     if (first < 0) {
       if (P->info.out_exact && l != P->frame_cap[f]) need_compact = true;
       from.push_back(P->frame_out[f]);
@@ -1611,8 +1655,10 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
   return ZD_OK;
 }
 
-int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
-  if (!P || (!src && n) || n != P->info.src_bytes) return ZD_E_INVALID_ARG;
+// One decode of plan P, host in / host out: the frames before the first
+// failure land in dst (up to cap bytes), *total = their length.
+static int plan_decompress_once(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
+                                uint64_t* total) {
   const uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
   // device buffers owned by the plan (kept for the next call), the input and
   // output through the pinned ring (chunked, the host copies on the worker
@@ -1629,13 +1675,12 @@ int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, s
   HIPCHK(hipStreamSynchronize(s));
   const auto t1 = std::chrono::steady_clock::now();
   int r = zd_decode_async(P, P->io_src, P->io_dst, ob, s);
-  uint64_t total = 0;
   int32_t first = -1;
-  if (!r) r = zd_plan_results(P, P->io_dst, s, nullptr, nullptr, &total, &first);
+  *total = 0;
+  if (!r) r = zd_plan_results(P, P->io_dst, s, nullptr, nullptr, total, &first);
   if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG || r == ZD_E_DST_TOO_SMALL) return r;
-  const int status = r;
   const auto t2 = std::chrono::steady_clock::now();
-  const size_t copy = (size_t)std::min<uint64_t>(total, cap);
+  const size_t copy = (size_t)std::min<uint64_t>(*total, cap);
   if (copy && dst)
     if (int e = io_d2h(dst, P->io_dst, copy, s, R, ev.e)) return e;
   const auto t3 = std::chrono::steady_clock::now();
@@ -1643,9 +1688,61 @@ int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, s
   P->info.io_h2d_ns = ns(t0, t1);
   P->info.io_decode_ns = ns(t1, t2);
   P->info.io_d2h_ns = ns(t2, t3);
-  if (out_len) *out_len = (size_t)total;
-  if (!status && total > cap) return ZD_E_DST_TOO_SMALL;
-  return status;
+  return r;
+}
+
+// Re-plans past a frame that reached a limit the host can lift: a frame that
+// decodes past the capacity its plan reserved (its Frame_Content_Size, or
+// 128 KiB per block -- the reference checks neither, decoding_context.rs:
+// 29-47, block.rs:50) is planned again from its own start with four times the
+// capacity (K4_MAX_FRAME_OUT at most); a K4J frame whose pointer jumping did
+// not converge is planned again on the streaming executor.  Each re-plan
+// covers the input from that frame on; its output follows the frames before.
+constexpr int LIMIT_RETRIES = 12;
+
+int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+  if (!P || (!src && n) || n != P->info.src_bytes) return ZD_E_INVALID_ARG;
+  uint64_t total = 0;
+  int st = plan_decompress_once(P, src, n, dst, cap, &total);
+  if (st == ZD_E_HIP || st == ZD_E_INVALID_ARG || st == ZD_E_DST_TOO_SMALL) return st;
+  uint64_t produced = total;
+  P->info.replans = 0;
+  zd_plan* cur = P;
+  size_t base = 0;                                 // cur's input starts at src + base
+  for (int k = 0; k < LIMIT_RETRIES && st == ZD_E_OUT_OF_DOMAIN && cur->limit_frame >= 0; k++) {
+    const size_t f = (size_t)cur->limit_frame;
+    const uint64_t old_cap = cur->frame_cap[f];
+    uint32_t flags = cur->flags;
+    uint64_t cap0 = 0;
+    if (cur->limit_stage == LS_CAPACITY) {
+      if (old_cap >= K4_MAX_FRAME_OUT) break;      // past the streaming executor's positions: out of domain
+      cap0 = std::min<uint64_t>(K4_MAX_FRAME_OUT, std::max<uint64_t>(4 * old_cap, old_cap + (1u << 20)));
+    } else {
+      flags = (flags & ~ZD_F_BLOCK_PARALLEL) | ZD_F_FRAME_SERIAL;
+      cap0 = old_cap;
+    }
+    const size_t at = base + (size_t)cur->frame(f).d.src_offset;
+    zd_plan* Q = nullptr;
+    const int r = plan_create(src + at, nullptr, n - at, flags, nullptr, &Q, cap0);
+    if (r) { st = r; break; }
+    P->info.replans++;
+    uint64_t t2 = 0;
+    const uint64_t room = cap > produced ? cap - produced : 0;
+    st = plan_decompress_once(Q, src + at, n - at, room ? dst + produced : nullptr, room, &t2);
+    if (cur != P) zd_plan_destroy(cur);
+    cur = Q;
+    base = at;
+    if (st == ZD_E_HIP || st == ZD_E_INVALID_ARG || st == ZD_E_DST_TOO_SMALL) break;
+    produced += t2;
+  }
+  if (cur != P) {
+    P->info.error_key = cur->info.error_key;
+    zd_plan_destroy(cur);
+  }
+  if (st == ZD_E_HIP || st == ZD_E_INVALID_ARG) return st;
+  if (out_len) *out_len = (size_t)produced;
+  if (!st && produced > cap) return ZD_E_DST_TOO_SMALL;
+  return st;
 }
 
 int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, uint32_t flags) {
@@ -1761,6 +1858,7 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   if (int r = ctx_input(c, src, n)) return r;
   const hipStream_t s = c->s;
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.huge, 0, 4, s));
   // prebuilt comp 0 carries the context's tables
   CompState pcs{};
   if (P->has_prebuilt) {

@@ -148,10 +148,10 @@ struct FwBits {
 // A table needs K1's large scratch (more than K1S_SYMS symbols, or a
 // Huffman-weight table deeper than AL 6): the block goes to the second pass.
 constexpr int K1_BIG = 1;
-// A Huffman-weight stream past 253 weights: the reference keeps decoding (and
-// may never stop: every remaining state can read 0 bits, huffman.rs:121-124),
-// which the GPU path does not follow -- out of domain at the tree's parse.
-constexpr int K1_OOD_PARSE = 2;
+// A Huffman-weight stream past 255 weights (only in non-conforming input):
+// the reference keeps every weight, its symbols wrapping as u8
+// (huffman.rs:161-175); the block goes to the third pass (zd_k_tables_huge).
+constexpr int K1_HUGE = 2;
 constexpr uint32_t K1S_SYMS = 64;
 
 // parse_fse_table (fse.rs:16-69); dist holds max_sym entries (256: all)
@@ -311,10 +311,107 @@ __device__ void lut_holes(uint16_t* lut, int p, uint32_t a, uint32_t b) {
   }
 }
 
+// Trees deeper than the LUT (maxBits p in 13..31, non-conforming input:
+// zstd encoders stop at 11) keep their codes as intervals of the p-bit code
+// space instead, in the LUT slot: dword 0 the group count G, then per code
+// width (longest first) {first code, end, width, offset of its symbols}, the
+// symbol bytes from byte DEEP_SYMS_AT.  The same insertion as the LUT fill
+// (from_number_of_bits + insert, huffman.rs:132-175): longest codes first,
+// each width's symbols ascending from the next aligned slot, a code that no
+// longer fits is dropped.  count(w) = symbols of width w, emit(w, k, dst)
+// writes the first k of them.  K2 decodes these blocks with huf_stream_deep.
+constexpr uint32_t DEEP_SYMS_AT = 512;
+constexpr uint32_t DEEP_SYM_CAP = LUT_ENTRIES * 2 - DEEP_SYMS_AT;
+template <typename COUNT, typename EMIT>
+__device__ int deep_build(uint32_t* tab, int p, COUNT count, EMIT emit) {
+  const uint64_t T = 1ull << p;
+  uint64_t pos = 0;
+  uint32_t G = 0, off = 0;
+  uint8_t* syms = (uint8_t*)tab + DEEP_SYMS_AT;
+  for (int w = p; w >= 1; w--) {
+    const uint32_t c = count(w);
+    if (!c) continue;
+    const uint64_t S = 1ull << (p - w);
+    const uint64_t al = (pos + S - 1) & ~(S - 1);
+    const uint64_t fit = (T - al) / S;
+    const uint32_t k = (uint32_t)(c < fit ? c : fit);
+    pos = al + k * S;
+    if (!k) continue;
+    if (off + k > DEEP_SYM_CAP) return ZD_E_OUT_OF_DOMAIN;   // (trees of > 7,680 leaves)
+    tab[1 + 4 * G] = (uint32_t)al;
+    tab[2 + 4 * G] = (uint32_t)pos;
+    tab[3 + 4 * G] = (uint32_t)w;
+    tab[4 + 4 * G] = off;
+    emit(w, k, syms + off);
+    off += k;
+    G++;
+  }
+  tab[0] = G;
+  return 0;
+}
+
+// parse_fse (huffman.rs:108-130): the weights of an FSE-compressed tree
+// description, two alternating FSE states sharing one table, each weight
+// handed to put(i, w) (put returns false: K1_HUGE, the weights do not fit the
+// pass's scratch).  The reference loops forever when every state left reads
+// 0 bits (huffman.rs:121-124); the oracle (zd_oracle.c h_parse_fse) calls
+// that a panic after guard_max weights, and so does this.
+template <typename LN, typename PUT>
+__device__ int k1_weight_stream(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, LN& L, PUT put,
+                                uint32_t* nw_out) {
+  const uint8_t h = desc[0];
+  FwBits fw{desc + 1, h, 0};
+  uint8_t al;
+  uint32_t nsym;
+  int st = parse_ncount(fw, &al, L.dist, &nsym, LN::SYMS);
+  if (!st && (1u << al) > LN::WFSE) st = K1_BIG;
+  if (!st) st = build_fse(al, L.dist, nsym, L.fse, L.sym, L.next);
+  BwBits bs;
+  if (!st) st = bs.init(desc + 1 + fw.bytes_read(), h - fw.bytes_read(), src, src_end);
+  uint32_t nw = 0;
+  if (!st) {
+    const uint64_t guard_max = (8 * (uint64_t)h + 2) * ((1u << al) + 2) * 2;
+    uint32_t sa = 0, sb = 0, v;
+    st = bs.take(al, &sa);
+    if (!st) st = bs.take(al, &sb);
+    bool last_updated_is_first = false, last_read_is_first = false;
+    bool has_a = true, has_b = true;
+    while (!st) {
+      const uint32_t cur = last_updated_is_first ? sb : sa;
+      const uint32_t nb = fse_nb(L.fse[cur], al);
+      if ((int64_t)nb > bs.bitpos) break;
+      if (nw >= guard_max) { st = ZD_E_REF_PANIC; break; }
+      uint32_t w;
+      if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
+      else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
+      if (!put(nw, w)) { st = K1_HUGE; break; }
+      nw++;
+      uint32_t& sx = last_updated_is_first ? sb : sa;
+      bool& has = last_updated_is_first ? has_b : has_a;
+      if (has) { st = ZD_E_REF_PANIC; break; }
+      st = bs.take((int)nb, &v);
+      if (st) break;
+      sx = fse_base(L.fse[sx], al) + v;
+      has = true;
+      last_updated_is_first = !last_updated_is_first;
+    }
+    for (int k = 0; k < 2 && !st; k++) {
+      uint32_t w;
+      if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
+      else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
+      if (!put(nw, w)) { st = K1_HUGE; break; }
+      nw++;
+    }
+  }
+  *nw_out = nw;
+  return st;
+}
+
 // HuffmanDecoder::parse + from_weights + from_number_of_bits (huffman.rs:
 // 80-203) -> LUT of 2^p u16 entries {symbol | width << 8}; entries no code
 // reaches get LUT_ABSENT | depth of the absent tree node.  Returns status;
-// *p_out = maxBits.
+// *p_out = maxBits.  A weight stream longer than the scratch (255 weights,
+// a tree of 256 symbols) returns K1_HUGE: the third pass takes the block.
 template <typename LN>
 __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, LN& L,
                                uint16_t* lut, int* p_out) {
@@ -322,46 +419,11 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
   uint32_t nw = 0;
   const uint8_t h = desc[0];
   if (h < 128) {
-    // parse_fse (huffman.rs:108-130): two alternating FSE states share one table
-    FwBits fw{desc + 1, h, 0};
-    uint8_t al;
-    uint32_t nsym;
-    st = parse_ncount(fw, &al, L.dist, &nsym, LN::SYMS);
-    if (!st && (1u << al) > LN::WFSE) st = K1_BIG;
-    if (!st) st = build_fse(al, L.dist, nsym, L.fse, L.sym, L.next);
-    BwBits bs;
-    if (!st) st = bs.init(desc + 1 + fw.bytes_read(), h - fw.bytes_read(), src, src_end);
-    if (!st) {
-      uint32_t sa = 0, sb = 0, v;
-      st = bs.take(al, &sa);
-      if (!st) st = bs.take(al, &sb);
-      bool last_updated_is_first = false, last_read_is_first = false;
-      bool has_a = true, has_b = true;
-      while (!st) {
-        const uint32_t cur = last_updated_is_first ? sb : sa;
-        const uint32_t nb = fse_nb(L.fse[cur], al);
-        if ((int64_t)nb > bs.bitpos) break;
-        uint32_t w;
-        if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
-        else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
-        if (nw >= K1_MAX_WEIGHTS - 2) { st = K1_OOD_PARSE; break; }
-        L.weights[nw++] = (uint8_t)w;
-        uint32_t& sx = last_updated_is_first ? sb : sa;
-        bool& has = last_updated_is_first ? has_b : has_a;
-        if (has) { st = ZD_E_REF_PANIC; break; }
-        st = bs.take((int)nb, &v);
-        if (st) break;
-        sx = fse_base(L.fse[sx], al) + v;
-        has = true;
-        last_updated_is_first = !last_updated_is_first;
-      }
-      for (int k = 0; k < 2 && !st; k++) {
-        uint32_t w;
-        if (last_read_is_first) { last_read_is_first = false; if (!has_b) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sb]); has_b = false; }
-        else { last_read_is_first = true; if (!has_a) { st = ZD_E_REF_PANIC; break; } w = fse_sym(L.fse[sa]); has_a = false; }
-        L.weights[nw++] = (uint8_t)w;
-      }
-    }
+    st = k1_weight_stream(desc, src, src_end, L, [&](uint32_t i, uint32_t w) {
+      if (i >= K1_MAX_WEIGHTS) return false;
+      L.weights[i] = (uint8_t)w;
+      return true;
+    }, &nw);
   } else {
     // parse_direct (huffman.rs:92-106): high nibble first
     nw = (uint32_t)h - 127;
@@ -391,9 +453,22 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
   for (uint32_t i = 0; i < nw; i++)
     if (L.weights[i] > (uint32_t)p + 1) return ZD_E_REF_PANIC;
   if (manquant > (uint32_t)p + 1) return ZD_E_REF_PANIC;
-  if (p > LUT_MAX_BITS) return ZD_E_OUT_OF_DOMAIN;
   L.weights[nw] = (uint8_t)manquant;          // the implied last symbol: width p + 1 - manquant
   const uint32_t n = nw + 1;
+  if (p > LUT_MAX_BITS) {
+    *p_out = p;
+    return deep_build((uint32_t*)lut, p,
+                      [&](int w) {
+                        uint32_t c = 0;
+                        for (uint32_t i = 0; i < n; i++) c += L.weights[i] && (int)(p + 1 - L.weights[i]) == w;
+                        return c;
+                      },
+                      [&](int w, uint32_t k, uint8_t* dst) {
+                        uint32_t r = 0;
+                        for (uint32_t i = 0; i < n && r < k; i++)
+                          if (L.weights[i] && (int)(p + 1 - L.weights[i]) == w) dst[r++] = (uint8_t)i;
+                      });
+  }
   // width(i) = weight ? p + 1 - weight : 0 (never inserted, huffman.rs:163-165)
   // from_number_of_bits + insert (huffman.rs:132-175): longest codes first,
   // ascending symbol, each at the leftmost free aligned slot; a code that no
@@ -491,7 +566,8 @@ template <bool BIG, int PART>
 __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restrict__ src, uint64_t src_size,
                                                         const CompBlock* __restrict__ comp, CompState* cstate,
                                                         FrameState* fstate, const uint32_t* __restrict__ list,
-                                                        uint32_t n_list, uint16_t* luts, uint16_t* fses) {
+                                                        uint32_t n_list, uint16_t* luts, uint16_t* fses,
+                                                        uint32_t* huge) {
   typedef typename std::conditional<BIG, K1Lane, K1LaneS>::type LN;
   __shared__ LN lanes[K1_LANES];
   const uint32_t li = blockIdx.x * K1_LANES + threadIdx.x;
@@ -509,11 +585,11 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
       cstate[ci].k1_bigh = 1;
       return;
     }
-    if (st == K1_OOD_PARSE) {
-      key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_HUF_DESC, 0, ZD_E_OUT_OF_DOMAIN));
-      return;
-    }
-    if (st == ZD_E_OUT_OF_DOMAIN) {
+    if (st == K1_HUGE) {
+      // the third pass builds this tree (its error, if any, sorts before the
+      // sequence tables' in key_min); Block::parse goes on to the sequences
+      huge[1 + atomicAdd(&huge[0], 1u)] = ci;
+    } else if (st == ZD_E_OUT_OF_DOMAIN) {
       // the tree parsed (the reference's Block::parse goes on to the
       // sequences section) but no GPU LUT holds it: out of domain where the
       // reference would decode these literals, after every parse error of
@@ -540,6 +616,123 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
     cstate[ci].bs_off = bo;
     cstate[ci].bs_size = bsz;
     if (st) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, (uint32_t)sub, st));
+  }
+}
+
+// Trees whose weight stream runs past 255 weights (non-conforming input):
+// one block per lane, four lanes per workgroup, a grid that walks the list
+// the first two passes appended to (huge[0] blocks).  The reference keeps
+// every weight: symbol i is `i as u8`, and from_number_of_bits sorts by
+// (width, symbol byte), so the tree depends only on how many weights of each
+// width each byte value has -- counted, not stored: one run of the weight
+// stream for from_weights' sum (huffman.rs:177-203), a second for the counts,
+// then the same LUT fill as k1_huffman_lane in (width desc, byte asc) order
+// (equal (width, byte) leaves are interchangeable).
+constexpr int K1H_LANES = 1, K1H_GRID = 64;
+struct K1LaneH {
+  static constexpr uint32_t SYMS = 256, WFSE = FSE_TAB;
+  uint16_t fse[FSE_TAB];
+  uint8_t sym[FSE_TAB];
+  uint16_t next[256];
+  int16_t dist[256];
+  uint32_t cnt[32][256];                          // weights per (code width, symbol byte)
+  uint32_t tot[32], start[32], placed[32];
+};
+
+__device__ int k1_huffman_huge(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, K1LaneH& L,
+                               uint16_t* lut, int* p_out) {
+  uint32_t sum = 0, maxw = 0, nw = 0;
+  bool panic = false;
+  int st = k1_weight_stream(desc, src, src_end, L, [&](uint32_t, uint32_t w) {
+    if (w) {
+      if (w - 1 >= 32 || sum > 0xFFFFFFFFu - (1u << (w - 1))) panic = true;
+      else sum += 1u << (w - 1);
+      maxw = w > maxw ? w : maxw;
+    }
+    return true;
+  }, &nw);
+  if (st) return st;
+  if (panic || sum == 0) return ZD_E_REF_PANIC;
+  int p = highbit32(sum);
+  if ((1ull << p) < sum) p++;
+  if (p >= 32) return ZD_E_REF_PANIC;
+  const uint8_t rest = (uint8_t)((1u << p) - sum);
+  if (rest == 0) return ZD_E_REF_PANIC;           // D3
+  const uint32_t manquant = (uint32_t)highbit32(rest) + 1;
+  if (maxw > (uint32_t)p + 1 || manquant > (uint32_t)p + 1) return ZD_E_REF_PANIC;
+  for (int w = 0; w <= p; w++)
+    for (int b = 0; b < 256; b++) L.cnt[w][b] = 0;
+  uint32_t nw2 = 0;
+  st = k1_weight_stream(desc, src, src_end, L, [&](uint32_t i, uint32_t w) {
+    if (w) L.cnt[p + 1 - w][i & 0xFF]++;
+    return true;
+  }, &nw2);
+  if (st) return st;
+  L.cnt[p + 1 - manquant][nw & 0xFF]++;          // the implied last symbol
+  if (p > LUT_MAX_BITS) {
+    *p_out = p;
+    return deep_build((uint32_t*)lut, p,
+                      [&](int w) {
+                        uint32_t t = 0;
+                        for (int b = 0; b < 256; b++) t += L.cnt[w][b];
+                        return t;
+                      },
+                      [&](int w, uint32_t k, uint8_t* dst) {
+                        uint32_t r = 0;
+                        for (int b = 0; b < 256 && r < k; b++)
+                          for (uint32_t c = L.cnt[w][b]; c > 0 && r < k; c--) dst[r++] = (uint8_t)b;
+                      });
+  }
+  const uint32_t T = 1u << p;
+  uint32_t pos = 0;
+  for (int w = p; w >= 1; w--) {
+    uint32_t t = 0;
+    for (int b = 0; b < 256; b++) t += L.cnt[w][b];
+    L.tot[w] = t;
+    if (!t) continue;
+    const uint32_t S = 1u << (p - w);
+    const uint32_t al = (pos + S - 1) & ~(S - 1);
+    lut_holes(lut, p, pos, al);
+    const uint32_t fit = (T - al) / S;
+    const uint32_t k = t < fit ? t : fit;
+    L.start[w] = al;
+    L.placed[w] = k;
+    pos = al + k * S;
+  }
+  lut_holes(lut, p, pos, T);
+  for (int w = p; w >= 1; w--) {
+    if (!L.tot[w]) continue;
+    const uint32_t S = 1u << (p - w);
+    uint32_t r = 0;
+    for (int b = 0; b < 256 && r < L.placed[w]; b++) {
+      const uint16_t ent = (uint16_t)(b | (lut_field((uint32_t)w, p) << 8));
+      for (uint32_t c = L.cnt[w][b]; c > 0 && r < L.placed[w]; c--, r++)
+        for (uint32_t e = 0; e < S; e++) lut[L.start[w] + r * S + e] = ent;
+    }
+  }
+  *p_out = p;
+  return 0;
+}
+
+__global__ __launch_bounds__(K1H_LANES) void zd_k_tables_huge(const uint8_t* __restrict__ src, uint64_t src_size,
+                                                              const CompBlock* __restrict__ comp, CompState* cstate,
+                                                              FrameState* fstate, const uint32_t* __restrict__ huge,
+                                                              uint16_t* luts) {
+  __shared__ K1LaneH lanes[K1H_LANES];
+  K1LaneH& L = lanes[threadIdx.x];
+  const uint32_t n = huge[0];
+  for (uint32_t k = blockIdx.x * K1H_LANES + threadIdx.x; k < n; k += gridDim.x * K1H_LANES) {
+    const uint32_t ci = huge[1 + k];
+    const CompBlock C = comp[ci];
+    int p = 0;
+    const int st = k1_huffman_huge(src + C.src + C.lit_data, src, src + src_size, L,
+                                   luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
+    if (st == ZD_E_OUT_OF_DOMAIN)
+      key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
+    else if (st)
+      key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_HUF_DESC, 0, st));
+    else
+      cstate[ci].huf_bits = (uint8_t)p;
   }
 }
 
@@ -793,6 +986,59 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
   return st;
 }
 
+// One stream of a deep tree (deep_build): symbol by symbol, the top p bits
+// (p <= 31) looked up in the slot's code intervals; a code that falls between
+// intervals is an absent tree node at the depth of the largest aligned block
+// of the gap around it (as lut_holes).  The reference's checks as in
+// huf_stream's tail.
+__device__ int huf_stream_deep(const uint8_t* bs, uint32_t size, uintptr_t base, const uint32_t* tab, int p,
+                               uint8_t* out, uint32_t cap, uint32_t* count_out) {
+  uint32_t count = 0;
+  *count_out = 0;
+  if (size == 0) return ZD_E_EMPTY_INPUT_DATA;
+  const uint8_t lastb = bs[size - 1];
+  if (lastb == 0) return ZD_E_NULL_BYTE;
+  int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
+  const uint32_t G = tab[0];
+  const uint8_t* syms = (const uint8_t*)tab + DEEP_SYMS_AT;
+  const uint64_t T = 1ull << p;
+  int st = 0;
+  while (pos > 0 && !st) {
+    const WinU w = winu_load(bs, base, pos);
+    uint32_t idx = (uint32_t)(winu_top(w, 0) >> (64 - p));
+    if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
+    uint64_t a = 0, b = T;
+    int32_t nb = -1;
+    uint8_t sym = 0;
+    for (uint32_t g = 0; g < G; g++) {
+      const uint32_t lo = tab[1 + 4 * g], hi = tab[2 + 4 * g];
+      if (idx < lo) { b = lo; break; }
+      if (idx < hi) {
+        nb = (int32_t)tab[3 + 4 * g];
+        sym = syms[tab[4 + 4 * g] + ((idx - lo) >> (p - nb))];
+        break;
+      }
+      a = hi;
+    }
+    if (nb < 0) {
+      int k = p;
+      for (; k > 0; k--) {
+        const uint64_t lo = (uint64_t)idx & ~((1ull << k) - 1);
+        if (lo >= a && lo + (1ull << k) <= b) break;
+      }
+      st = p - k <= pos ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
+    } else if (nb > pos) {
+      st = ZD_E_NOT_ENOUGH_BITS;
+    } else {
+      pos -= nb;
+      if (count < cap) out[count] = sym;
+      count++;
+    }
+  }
+  *count_out = count;
+  return st;
+}
+
 __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restrict__ src,
                                                          const CompBlock* __restrict__ comp, CompState* cstate,
                                                          FrameState* fstate, const uint32_t* __restrict__ list,
@@ -842,10 +1088,16 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint32_t cap = k < m - 1 ? seg : (R > start ? R - start : 0);
     const uint8_t* blk = src + C.src;
     const uintptr_t lo = (uintptr_t)src;
-    uint8_t* slack = lits + C.lit_out + R + 8;       // the block's literal slot has 16 bytes past R
+    // the block's literal slot: R + 16 + lit_extra bytes of literals (the
+    // streams laid back-to-back may run past R), then 8 bytes of slack that
+    // the fast loops' placeholder stores hit (never read)
+    uint8_t* slack = lits + C.lit_out + R + 16 + C.lit_extra;
     uint32_t count;
     int st;
-    if (use_lds)
+    if (p > LUT_MAX_BITS)
+      st = huf_stream_deep(blk + off, C.stream_size[k], lo, (const uint32_t*)g, p, lits + C.lit_out + start, cap,
+                           &count);
+    else if (use_lds)
       st = huf_stream<const lds_u16*>(blk + off, C.stream_size[k], lo, (const lds_u16*)lut[b], p,
                                       lits + C.lit_out + start, cap, &count, slack);
     else
@@ -872,9 +1124,10 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
       redo_at[b][j] = total;
       total += counts[b][j];
     }
-    const bool fits = total <= R + 16;          // the block's literal slot (host: R + 16 bytes)
+    const bool fits = total <= R + 16 + C.lit_extra;   // the block's literal slot
     if (!rfc && !err && !fits)
-      key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
+      key_min(fstate, C.frame,
+              make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, DS_LIT_OVERFLOW_SUB, ZD_E_OUT_OF_DOMAIN));
     redo[b] = !rfc && !err && fits;
     cstate[ci].lit_count = total;
     if (err || (!rfc && !fits)) cstate[ci].stop = 1;
@@ -886,13 +1139,16 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint8_t* blk = src + C.src;
     uint32_t count;
     const uint32_t at = redo_at[b][k];
-    if (use_lds)
+    if (p > LUT_MAX_BITS)
+      (void)huf_stream_deep(blk + off, C.stream_size[k], (uintptr_t)src, (const uint32_t*)g, p, lits + C.lit_out + at,
+                            counts[b][k], &count);
+    else if (use_lds)
       (void)huf_stream<const lds_u16*>(blk + off, C.stream_size[k], (uintptr_t)src,
                                        (const lds_u16*)lut[b], p, lits + C.lit_out + at, counts[b][k], &count,
-                                       lits + C.lit_out + R + 8);
+                                       lits + C.lit_out + R + 16 + C.lit_extra);
     else
       (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)src, (g_u16*)g, p,
-                               lits + C.lit_out + at, counts[b][k], &count, lits + C.lit_out + R + 8);
+                               lits + C.lit_out + at, counts[b][k], &count, lits + C.lit_out + R + 16 + C.lit_extra);
   }
 }
 
@@ -1805,11 +2061,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
     if (B.type == 5) continue;
     if (B.type == 0 || B.type == 4) {
-      if (!k4_emit_lits(X, src + B.src, 0, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN);
+      if (!k4_emit_lits(X, src + B.src, 0, B.size)) err_key = make_key(PH_LIMIT, j, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN);
       continue;
     }
     if (B.type == 1) {
-      if (!k4_emit_lits(X, nullptr, B.rle, B.size)) err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN);
+      if (!k4_emit_lits(X, nullptr, B.rle, B.size)) err_key = make_key(PH_LIMIT, j, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN);
       continue;
     }
     const CompBlock C = comp[B.comp];
@@ -2014,7 +2270,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         }
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
         const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
-        if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN); break; }
+        if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, s0, ZD_E_OUT_OF_DOMAIN); break; }
         const bool act = (uint32_t)lane < k;
         k4_sync();                               // staged literals visible
         // literals (every lane its own run; from the stage when it holds them)
@@ -2107,7 +2363,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         // one sequence larger than the window's room: the whole wave copies it
         if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, bll) ||
             !k4_emit_match(X, (l_u8*)pat, (uint32_t)(boff < 0xFFFFFFFFull ? boff : 0xFFFFFFFFull), bml)) {
-          err_key = make_key(PH_LIMIT, j, DS_EXECUTE, s0, ZD_E_OUT_OF_DOMAIN);
+          err_key = make_key(PH_LIMIT, j, LS_CAPACITY, s0, ZD_E_OUT_OF_DOMAIN);
           break;
         }
         lit_cursor += bll;
@@ -2117,7 +2373,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     if (err_key != KEY_NONE) break;
     // leftover literals (decoding_context.rs:101-103)
     if (lit_cursor < nl && !k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, nl - lit_cursor))
-      err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_OUT_OF_DOMAIN);
+      err_key = make_key(PH_LIMIT, j, LS_CAPACITY, n, ZD_E_OUT_OF_DOMAIN);
   }
   if (err_key != KEY_NONE) {
     if (lane == 0) key_min(fstate, f, err_key);
@@ -2283,7 +2539,7 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
     if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
     if (B.type == 5) continue;
     if (B.type != 2) {                            // raw / RLE / skippable payload
-      if ((uint64_t)pos + B.size > cap) { err_key = make_key(PH_LIMIT, j, 0, 0, ZD_E_OUT_OF_DOMAIN); break; }
+      if ((uint64_t)pos + B.size > cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN); break; }
       const uint32_t fill = B.rle * 0x01010101u;
       const u32x4 f4 = (u32x4){fill, fill, fill, fill};
       for (uint32_t x = 16 * t; x < B.size; x += 16 * K4F_T) {
@@ -2450,7 +2706,7 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
       __syncthreads();
       if (L.err != ~0ull || L.lim != ~0ull) {
         if (L.err != ~0ull) err_key = make_key(PH_DECODE, j, DS_EXECUTE, (uint32_t)(L.err >> 8), -(int)(L.err & 0xFF));
-        else err_key = make_key(PH_LIMIT, j, DS_EXECUTE, (uint32_t)L.lim, ZD_E_OUT_OF_DOMAIN);
+        else err_key = make_key(PH_LIMIT, j, LS_CAPACITY, (uint32_t)L.lim, ZD_E_OUT_OF_DOMAIN);
         break;
       }
 #ifdef ZD_K4F_PROF
@@ -2555,7 +2811,7 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
     // leftover literals (decoding_context.rs:101-103)
     if (lit_cursor < nl) {
       const uint32_t rest = nl - lit_cursor;
-      if ((uint64_t)pos + rest > cap) { err_key = make_key(PH_LIMIT, j, DS_EXECUTE, n, ZD_E_OUT_OF_DOMAIN); break; }
+      if ((uint64_t)pos + rest > cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, n, ZD_E_OUT_OF_DOMAIN); break; }
       for (uint32_t x = 16 * t; x < rest; x += 16 * K4F_T) {
         const u32x4 v = lsrc ? ldg16(lsrc + lit_cursor + x) : f4;
         sts_n((l_u8*)L.buf + pos + x, v, min(16u, rest - x));
@@ -2868,7 +3124,7 @@ __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__
     const uint64_t om = __ballot(live && pos + incl > cap);
     if (om) {
       const int fo = __ffsll((long long)om) - 1;
-      if (lane == fo) key_min(fstate, JF.frame, make_key(PH_LIMIT, jd[e].j, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
+      if (lane == fo) key_min(fstate, JF.frame, make_key(PH_LIMIT, jd[e].j, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN));
       if (lane >= fo) { live = false; size = 0; m[0] = jr_sym(0); m[1] = jr_sym(1); m[2] = jr_sym(2); }
       incl = wave_scan_u64(size, lane);
     }
@@ -3124,7 +3380,7 @@ __device__ inline bool j_piece(uint8_t* outbase, const FrameDesc* __restrict__ f
   }
   if (changed) j_store_words(st + p0, w, nb);
   if (pm) {
-    if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, DS_EXECUTE, 0, ZD_E_OUT_OF_DOMAIN));
+    if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, LS_JROUNDS, 0, ZD_E_OUT_OF_DOMAIN));
     return true;
   }
   u32x4 v = (u32x4){0u, 0u, 0u, 0u};
@@ -3261,18 +3517,24 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
   }
-  auto k1 = [&](auto pass_small, auto pass_big, hipStream_t st) {
+  auto* huge = (uint32_t*)(ws + W.huge);
+  auto k1 = [&](auto pass_small, auto pass_big, hipStream_t st, bool huf) {
     const dim3 g((a.n_tables + K1_LANES - 1) / K1_LANES), b(K1_LANES);
     const uint32_t* lt = (const uint32_t*)(ws + W.list_tables);
-    hipLaunchKernelGGL(pass_small, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses);
-    hipLaunchKernelGGL(pass_big, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses);
+    hipLaunchKernelGGL(pass_small, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses,
+                       huge);
+    hipLaunchKernelGGL(pass_big, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses,
+                       huge);
+    if (huf)                                   // the trees of more than 256 symbols the two passes listed
+      hipLaunchKernelGGL(zd_k_tables_huge, dim3(K1H_GRID), dim3(K1H_LANES), 0, st, a.src, a.src_size, comp, cstate,
+                         fstate, (const uint32_t*)huge, luts);
   };
   if (a.n_tables) {
     if (fork) {
-      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2);
-      k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s);
+      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
+      k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
     } else {
-      k1(zd_k_tables<false, 3>, zd_k_tables<true, 3>, s);
+      k1(zd_k_tables<false, 3>, zd_k_tables<true, 3>, s, true);
     }
   }
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;

@@ -44,7 +44,8 @@ class PlanInfo(C.Structure):
                 ("workspace_bytes", C.c_uint64), ("nsequences", C.c_uint64), ("nliterals", C.c_uint64),
                 ("index_status", C.c_int32), ("_pad", C.c_uint32), ("host_ns", C.c_uint64),
                 ("device_ns", C.c_uint64), ("walk_serial_bytes", C.c_uint64),
-                ("io_h2d_ns", C.c_uint64), ("io_decode_ns", C.c_uint64), ("io_d2h_ns", C.c_uint64)]
+                ("io_h2d_ns", C.c_uint64), ("io_decode_ns", C.c_uint64), ("io_d2h_ns", C.c_uint64),
+                ("error_key", C.c_uint64), ("replans", C.c_uint64)]
 
 
 class GatherResult(C.Structure):

@@ -26,35 +26,38 @@ def frames_index(data: bytes, max_frames: int = 0):
     return frames, blocks, st, cons.value
 
 
-def decompress(data: bytes, print_skippable: bool = False) -> bytes:
-    """Decode every frame of `data` on the GPU (host in, host out)."""
+def _decompress(data: bytes, flags: int):
+    """zd_decompress into a buffer sized from the plan; again with the size it
+    reports when the output came out larger (a frame that decodes past its
+    declared size is re-planned inside zd_plan_decompress)."""
     L = _lib.lib()
     p, n, keep = _lib.buf(data)
-    # size the output from the plan (exact when every frame carries its FCS)
-    plan = Plan(data, print_skippable)
+    plan = Plan(data, bool(flags & _lib.F_SKIPPABLE), flags & ~_lib.F_SKIPPABLE)
     cap = max(plan.info.out_bytes, 1)
     plan.close()
-    out = (C.c_uint8 * cap)()
-    ol = C.c_size_t()
-    st = L.zd_decompress(p, n, out, cap, C.byref(ol), _lib.F_SKIPPABLE if print_skippable else 0)
+    for _ in range(2):
+        out = (C.c_uint8 * cap)()
+        ol = C.c_size_t()
+        st = L.zd_decompress(p, n, out, cap, C.byref(ol), flags)
+        if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
+            _lib.check(st, "zd_decompress")
+        if ol.value <= cap:
+            break
+        cap = ol.value
+    return st, bytes(out[: min(ol.value, cap)])
+
+
+def decompress(data: bytes, print_skippable: bool = False) -> bytes:
+    """Decode every frame of `data` on the GPU (host in, host out)."""
+    st, out = _decompress(data, _lib.F_SKIPPABLE if print_skippable else 0)
     _lib.check(st, "zd_decompress")
-    return bytes(out[: ol.value])
+    return out
 
 
 def decompress_status(data: bytes, print_skippable: bool = False, flags: int = 0):
     """(status, output of the frames before the first failure).  flags: extra
     zd_plan flags (_lib.F_BLOCK_PARALLEL / F_FRAME_SERIAL pick the executor)."""
-    L = _lib.lib()
-    p, n, keep = _lib.buf(data)
-    plan = Plan(data, print_skippable, flags)
-    cap = max(plan.info.out_bytes, 1)
-    plan.close()
-    out = (C.c_uint8 * cap)()
-    ol = C.c_size_t()
-    st = L.zd_decompress(p, n, out, cap, C.byref(ol), (_lib.F_SKIPPABLE if print_skippable else 0) | flags)
-    if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
-        _lib.check(st, "zd_decompress")
-    return st, bytes(out[: min(ol.value, cap)])
+    return _decompress(data, (_lib.F_SKIPPABLE if print_skippable else 0) | flags)
 
 
 class Plan:
