@@ -289,6 +289,8 @@ def main():
     ap.add_argument("--gather", choices=["auto", "on", "off"], default="auto",
                     help="N>1: time gathering every rank's output to rank 0 over RCCL, reported apart "
                          "(auto: on for strong scaling)")
+    ap.add_argument("--no-host-io", action="store_true",
+                    help="skip the host-in / host-out leg (profiling runs of the device path)")
     ap.add_argument("--experiment", action="store_true",
                     help="timing-only variants: do not stop on decode errors")
     args = ap.parse_args()
@@ -490,7 +492,7 @@ def main():
     # host through pinned chunks, plan-owned device buffers (rank 0 only, the
     # other ranks wait: one PCIe link measured alone)
     host_io = None
-    if rank == 0 and not args.experiment:
+    if rank == 0 and not args.experiment and not args.no_host_io:
         host_io = host_io_leg(plan, data, info, src if not strong else ref_bytes, reps if not strong else 1)
         del plan_io_scratch[:]
     if dist:
@@ -555,7 +557,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic_of(dom, args, world),
-                "traffic_unit": "GB per launch (rocprofv3 FETCH_SIZE + WRITE_SIZE, uncorrected, profiles/traffic.json)",
+                "traffic_unit": "GB per launch (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE, the x2 calibrated on K4's own "
+                                "access patterns: profiles/r3_fetch_calibration.txt; profiles/traffic.json)",
                 "traffic_commit": traffic_commit(),
                 "alg_bytes_per_launch": int(alg_per_launch),
                 "pipeline_achieved": round(alg_per_launch / (ms_per_step / 1e3) / 1e9, 1),

@@ -276,6 +276,34 @@ def test_one_lane_k3_chain(resources):
             assert_parity(bytes(d), False, f"flags={flags} corrupt #{it}", flags=flags)
 
 
+def test_chain_groups():
+    """Plans whose K3 chains fit one round run as chain groups by default
+    (frames by their longest chain, each group's K3 -> K4 / K4F on its own
+    stream); ZD_F_NO_GROUPS keeps one K3 launch, then K4.  Both against the
+    oracle: a 300-frame plan (K4F) of frames of unequal chain lengths, a
+    1,200-frame plan (streaming K4) with multi-block frames and a frame of
+    20 blocks (K4J after the groups join), and corruptions inside both."""
+    from zstd_decompressor import _lib
+    r = random.Random(83)
+    frames = []
+    for i in range(300):
+        n = r.choice([2048, 8192, 32768, 96 << 10])
+        frames.append(gen.frames(gen.text(n, seed=1000 + i), 1 << 20, r.choice([1, 3, 9])))
+    k4f_plan = b"".join(frames)
+    parts = [gen.frames(gen.text(6000 + 37 * i, seed=2000 + i), 4096, 3) for i in range(1200)]
+    parts.insert(600, gen.frames(gen.text(3 << 20, seed=17), 3 << 20, 3))   # 24 blocks: K4J
+    parts.insert(100, gen.frames(gen.text(1 << 20, seed=18), 1 << 20, 9))
+    k4_plan = b"".join(parts)
+    for flags in (_lib.F_NO_GROUPS, 0):
+        for name, data in (("k4f plan", k4f_plan), ("k4 plan", k4_plan)):
+            assert_parity(data, False, f"flags={flags} {name}", flags=flags)
+            for it in range(6):
+                d = bytearray(data)
+                for _ in range(r.randrange(1, 4)):
+                    d[r.randrange(len(d))] = r.randrange(256)
+                assert_parity(bytes(d), False, f"flags={flags} {name} corrupt #{it}", flags=flags)
+
+
 def test_plan_decompress_reuses_the_plan(resources):
     """zd_plan_decompress: host in / host out with a plan made once (the
     INTEGRATION.md decompress() pattern), equal to the oracle's output."""
