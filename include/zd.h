@@ -151,10 +151,6 @@ typedef struct zd_plan zd_plan;
 /* Sequence-decode choice: K3 with one lane per block instead of four (the
  * default, K3Q).  Same records either way; tests run both. */
 #define ZD_F_SEQ_ONE_LANE   8u
-/* Launch order: one K3 launch, then K4, instead of chain groups (plans whose
- * K3 chains fit one round: each group's K3 -> K4 on its own stream, DESIGN.md
- * §4).  Same output either way; tests run both. */
-#define ZD_F_NO_GROUPS     16u
 
 typedef struct zd_plan_info {
   uint64_t nframes;        /* frames in the plan (skippable included) */

@@ -276,14 +276,11 @@ def test_one_lane_k3_chain(resources):
             assert_parity(bytes(d), False, f"flags={flags} corrupt #{it}", flags=flags)
 
 
-def test_chain_groups():
-    """Plans whose K3 chains fit one round run as chain groups by default
-    (frames by their longest chain, each group's K3 -> K4 / K4F on its own
-    stream); ZD_F_NO_GROUPS keeps one K3 launch, then K4.  Both against the
-    oracle: a 300-frame plan (K4F) of frames of unequal chain lengths, a
-    1,200-frame plan (streaming K4) with multi-block frames and a frame of
-    20 blocks (K4J after the groups join), and corruptions inside both."""
-    from zstd_decompressor import _lib
+def test_mixed_frame_plans():
+    """Plans mixing frame sizes, levels and executors against the oracle: 300
+    frames of 2-96 KiB at levels 1/3/9 (K4F), and 1,200 runs of 4 KiB frames
+    (streaming K4) with a 1 MiB multi-block frame and a frame of 24 blocks
+    (K4J), each clean and with corruptions."""
     r = random.Random(83)
     frames = []
     for i in range(300):
@@ -294,14 +291,13 @@ def test_chain_groups():
     parts.insert(600, gen.frames(gen.text(3 << 20, seed=17), 3 << 20, 3))   # 24 blocks: K4J
     parts.insert(100, gen.frames(gen.text(1 << 20, seed=18), 1 << 20, 9))
     k4_plan = b"".join(parts)
-    for flags in (_lib.F_NO_GROUPS, 0):
-        for name, data in (("k4f plan", k4f_plan), ("k4 plan", k4_plan)):
-            assert_parity(data, False, f"flags={flags} {name}", flags=flags)
-            for it in range(6):
-                d = bytearray(data)
-                for _ in range(r.randrange(1, 4)):
-                    d[r.randrange(len(d))] = r.randrange(256)
-                assert_parity(bytes(d), False, f"flags={flags} {name} corrupt #{it}", flags=flags)
+    for name, data in (("k4f plan", k4f_plan), ("k4 plan", k4_plan)):
+        assert_parity(data, False, name)
+        for it in range(6):
+            d = bytearray(data)
+            for _ in range(r.randrange(1, 4)):
+                d[r.randrange(len(d))] = r.randrange(256)
+            assert_parity(bytes(d), False, f"{name} corrupt #{it}")
 
 
 def test_plan_decompress_reuses_the_plan(resources):

@@ -443,7 +443,6 @@ struct JSegDesc {          // static: the scatter's work list
 struct Workspace {
   uint64_t comp, comp_state, blocks, frames, frame_state, frame_state0;
   uint64_t list_tables, list_huf, list_seq, list_k4f;   // u32 work lists
-  uint64_t list_seq_g, list_k4_g, list_k4f_g;           // the same lists by chain group (zd_host.cpp build_plan)
   uint64_t copies;                                      // CopyDesc[] for K0
   uint64_t lits, seqs, luts, fses;
   uint64_t jframes, jblkd, jblk, jseg, jsegd, jpend;    // K4J descriptors / state / round counters

@@ -63,9 +63,6 @@ struct zd_plan {
   std::vector<FrameDesc> fdesc;
   std::vector<FrameState> fstate0;
   std::vector<uint32_t> list_tables, list_huf, list_seq, list_k4f;
-  std::vector<uint32_t> list_seq_g, list_k4_g, list_k4f_g;   // by chain group (build_plan)
-  uint32_t n_groups = 0;                // chain groups (0: one K3 launch, then K4)
-  uint32_t g_seq[MAX_GROUPS + 1] = {}, g_k4[MAX_GROUPS + 1] = {}, g_k4f[MAX_GROUPS + 1] = {};
   std::vector<CopyDesc> copies;         // K0 pieces
   std::vector<JFrame> jframes;          // K4J frames, their blocks and the scatter's segments
   std::vector<JBlkDesc> jblkd;
@@ -85,7 +82,7 @@ struct zd_plan {
   uint64_t ws_bytes = 0;                 // size of the d_ws allocation (>= W.total: a cached block)
   int dev = -1;                          // the device d_ws and the aux stream belong to (upload_plan)
   uint64_t desc_bytes = 0;               // the host-filled head of the workspace (one upload)
-  uint8_t* d_staging = nullptr;          // when the output layout is not exact
+  uint8_t* d_staging = nullptr;          // the output of a non-exact layout, or the copy an exact one is compacted from
   uint64_t staging_bytes = 0;
   int index_status = 0;
   uint64_t cap0 = 0;                     // capacity of frame 0 instead of its own (a re-plan, zd_plan_decompress)
@@ -114,8 +111,6 @@ struct zd_plan {
   // second stream for K2 beside K3 (created on first launch)
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
-  hipStream_t gs[MAX_GROUPS - 1] = {};  // chain groups 1.. (group 0 runs on the caller's stream)
-  hipEvent_t gev[MAX_GROUPS] = {};
   // output layout of the last zd_plan_results (frames before the first failure)
   std::vector<uint64_t> res_off, res_len;
   uint64_t* d_meta = nullptr;            // zd_plan_results' compaction / zd_plan_checksums' arrays
@@ -189,7 +184,6 @@ struct Sink {
   FrameDesc* fdesc;
   FrameState* fstate0;
   uint32_t *list_tables, *list_huf, *list_seq, *list_k4f;
-  uint32_t *list_seq_g, *list_k4_g, *list_k4f_g;
   CopyDesc* copies;
   JFrame* jframes;
   JBlkDesc* jblkd;
@@ -487,20 +481,6 @@ size_t k3_slots() {
   return slots;
 }
 
-// Chain groups for plans whose K3 chains fit one round of the K3 slots: K3
-// time is then the longest chain, and one K4 launch after K3 leaves every
-// frame waiting for it.  Frames go to groups by their longest chain, each
-// group's K3 -> K4 on its own stream (launch_pipeline).  ZD_GROUPS=n forces n
-// groups (1: off) wherever the plan allows.
-constexpr size_t GROUP_MIN_SEQ_BLOCKS = 256;
-constexpr uint32_t GROUPS_DEFAULT = 3;
-uint32_t chain_groups(uint64_t n_seq, uint64_t n_frames, uint64_t out_len0) {
-  static const char* env = getenv("ZD_GROUPS");
-  const uint32_t want = env ? (uint32_t)std::max(1, std::min((int)MAX_GROUPS, atoi(env))) : GROUPS_DEFAULT;
-  if (want < 2 || out_len0 || n_seq < GROUP_MIN_SEQ_BLOCKS || n_seq > k3_slots() || n_frames < 2 * want) return 1;
-  return want;
-}
-
 // Builds device-side descriptors from the host frames: one counting pass and
 // one filling pass over the parts in parallel (each part's entries start at
 // the counts of the parts before it), then the K4J descriptors in frame order.
@@ -554,12 +534,6 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.list_huf = carve(4 * std::max<uint64_t>(T.huf, 1));
   W.list_seq = carve(4 * std::max<uint64_t>(T.seq, 1));
   W.list_k4f = carve(4 * std::max<uint64_t>(T.k4f, 1));
-  // chain groups: a plan whose K3 chains fit one round
-  const uint32_t G = (P->flags & ZD_F_NO_GROUPS) ? 1 : chain_groups(T.seq, T.frames, out_len0);
-  const bool grp = G > 1;
-  W.list_seq_g = carve(grp ? 4 * T.seq : 0);
-  W.list_k4_g = carve(grp ? 4 * T.frames : 0);
-  W.list_k4f_g = carve(grp ? 4 * std::max<uint64_t>(T.k4f, 1) : 0);
   W.copies = carve(sizeof(CopyDesc) * std::max<uint64_t>(T.copies, 1));
   W.jframes = carve(sizeof(JFrame) * std::max<uint64_t>(T.jframes, 1));
   W.jblkd = carve(sizeof(JBlkDesc) * std::max<uint64_t>(T.jblk, 1));
@@ -591,12 +565,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     uint8_t* b = H.p;
     S = Sink{(CompBlock*)(b + W.comp), (BlockRec*)(b + W.blocks), (FrameDesc*)(b + W.frames),
              (FrameState*)(b + W.frame_state0), (uint32_t*)(b + W.list_tables), (uint32_t*)(b + W.list_huf),
-             (uint32_t*)(b + W.list_seq), (uint32_t*)(b + W.list_k4f), (uint32_t*)(b + W.list_seq_g),
-             (uint32_t*)(b + W.list_k4_g), (uint32_t*)(b + W.list_k4f_g), (CopyDesc*)(b + W.copies),
+             (uint32_t*)(b + W.list_seq), (uint32_t*)(b + W.list_k4f), (CopyDesc*)(b + W.copies),
              (JFrame*)(b + W.jframes), (JBlkDesc*)(b + W.jblkd), (JSegDesc*)(b + W.jsegd), nullptr, nullptr};
     P->comps.clear(); P->blocks.clear(); P->fdesc.clear(); P->fstate0.clear();
     P->list_tables.clear(); P->list_huf.clear(); P->list_seq.clear(); P->list_k4f.clear(); P->copies.clear();
-    P->list_seq_g.clear(); P->list_k4_g.clear(); P->list_k4f_g.clear();
     P->jframes.clear(); P->jblkd.clear(); P->jsegd.clear();
   } else {
     P->comps.assign(T.comps, CompBlock{});
@@ -611,12 +583,8 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     P->jframes.assign(T.jframes, JFrame{});
     P->jblkd.assign(T.jblk, JBlkDesc{});
     P->jsegd.assign(T.jseg, JSegDesc{});
-    P->list_seq_g.assign(grp ? T.seq : 0, 0);
-    P->list_k4_g.assign(grp ? T.frames : 0, 0);
-    P->list_k4f_g.assign(grp ? T.k4f : 0, 0);
     S = Sink{P->comps.data(), P->blocks.data(), P->fdesc.data(), P->fstate0.data(), P->list_tables.data(),
-             P->list_huf.data(), P->list_seq.data(), P->list_k4f.data(), P->list_seq_g.data(), P->list_k4_g.data(),
-             P->list_k4f_g.data(), P->copies.data(), P->jframes.data(),
+             P->list_huf.data(), P->list_seq.data(), P->list_k4f.data(), P->copies.data(), P->jframes.data(),
              P->jblkd.data(), P->jsegd.data(), nullptr, nullptr};
   }
   S.frame_out = P->frame_out.data();
@@ -659,35 +627,6 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
       j_pieces += (fd.out_cap + 15) / 16;
       S.jframes[nj++] = jf;
     }
-  }
-
-  P->n_groups = 0;
-  if (grp) {
-    // a frame's K3 time is its longest block's chain: frames by that length,
-    // G groups of equal frame counts (shortest chains first), plan order
-    // inside a group (locality of the bitstreams, records and outputs)
-    std::vector<uint32_t> key(T.frames, 0);
-    for (uint64_t i = 0; i < T.seq; i++) {
-      const CompBlock& cb = S.comps[S.list_seq[i]];
-      key[cb.frame] = std::max(key[cb.frame], cb.nseq);
-    }
-    std::vector<uint32_t> ord(T.frames);
-    for (uint32_t f = 0; f < T.frames; f++) ord[f] = f;
-    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return key[x] < key[y]; });
-    std::vector<uint8_t> gof(T.frames);
-    for (uint64_t r = 0; r < T.frames; r++) gof[ord[r]] = (uint8_t)(r * G / T.frames);
-    uint32_t ns = 0, n4 = 0, nf = 0;
-    for (uint32_t g = 0; g < G; g++) {
-      P->g_seq[g] = ns; P->g_k4[g] = n4; P->g_k4f[g] = nf;
-      for (uint64_t i = 0; i < T.seq; i++)
-        if (gof[S.comps[S.list_seq[i]].frame] == g) S.list_seq_g[ns++] = S.list_seq[i];
-      for (uint32_t f = 0; f < T.frames; f++)
-        if (gof[f] == g && S.fdesc[f].lds == 0) S.list_k4_g[n4++] = f;
-      for (uint64_t i = 0; i < T.k4f; i++)
-        if (gof[S.list_k4f[i]] == g) S.list_k4f_g[nf++] = S.list_k4f[i];
-    }
-    P->g_seq[G] = ns; P->g_k4[G] = n4; P->g_k4f[G] = nf;
-    P->n_groups = G;
   }
 
   W.comp_state = carve(sizeof(CompState) * std::max<uint64_t>(T.comps, 1));
@@ -844,9 +783,6 @@ int upload_plan(zd_plan* P) {
         {W.list_huf, P->list_huf.data(), P->list_huf.size() * 4},
         {W.list_seq, P->list_seq.data(), P->list_seq.size() * 4},
         {W.list_k4f, P->list_k4f.data(), P->list_k4f.size() * 4},
-        {W.list_seq_g, P->list_seq_g.data(), P->list_seq_g.size() * 4},
-        {W.list_k4_g, P->list_k4_g.data(), P->list_k4_g.size() * 4},
-        {W.list_k4f_g, P->list_k4f_g.data(), P->list_k4f_g.size() * 4},
         {W.copies, P->copies.data(), P->copies.size() * sizeof(CopyDesc)},
         {W.jframes, P->jframes.data(), P->jframes.size() * sizeof(JFrame)},
         {W.jblkd, P->jblkd.data(), P->jblkd.size() * sizeof(JBlkDesc)},
@@ -864,13 +800,7 @@ int upload_plan(zd_plan* P) {
 
 // A plan's second stream and its fork/join events, kept for the next plans
 // of the process (creating them took ~0.25 ms per plan).
-struct AuxSet {
-  int dev;
-  hipStream_t s;
-  hipEvent_t fork, join;
-  hipStream_t gs[MAX_GROUPS - 1];         // chain-group streams and events
-  hipEvent_t gev[MAX_GROUPS];
-};
+struct AuxSet { int dev; hipStream_t s; hipEvent_t fork, join; };
 std::mutex& aux_mutex() {
   static std::mutex m;
   return m;
@@ -888,33 +818,20 @@ bool aux_take(zd_plan* P) {
     for (size_t i = 0; i < v.size(); i++) {
       if (v[i].dev != dev) continue;
       P->aux = v[i].s; P->fork = v[i].fork; P->join = v[i].join;
-      for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) P->gs[k] = v[i].gs[k];
-      for (uint32_t k = 0; k < MAX_GROUPS; k++) P->gev[k] = v[i].gev[k];
       v.erase(v.begin() + (long)i);
       return true;
     }
   }
-  bool ok = hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&P->fork, hipEventDisableTiming) == hipSuccess &&
-            hipEventCreateWithFlags(&P->join, hipEventDisableTiming) == hipSuccess;
-  for (uint32_t k = 0; ok && k + 1 < MAX_GROUPS; k++)
-    ok = hipStreamCreateWithFlags(&P->gs[k], hipStreamNonBlocking) == hipSuccess;
-  for (uint32_t k = 0; ok && k < MAX_GROUPS; k++)
-    ok = hipEventCreateWithFlags(&P->gev[k], hipEventDisableTiming) == hipSuccess;
-  return ok;
+  return hipStreamCreateWithFlags(&P->aux, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&P->fork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&P->join, hipEventDisableTiming) == hipSuccess;
 }
 void aux_give(zd_plan* P) {
   const int dev = P->dev;                 // the plan's device, not the current one
-  bool whole = P->aux && P->fork && P->join && dev >= 0;
-  for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) whole = whole && P->gs[k];
-  for (uint32_t k = 0; k < MAX_GROUPS; k++) whole = whole && P->gev[k];
-  if (whole) {
+  if (P->aux && P->fork && P->join && dev >= 0) {
     std::lock_guard<std::mutex> g(aux_mutex());
     if (aux_free().size() < 8) {
-      AuxSet a{dev, P->aux, P->fork, P->join, {}, {}};
-      for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) { a.gs[k] = P->gs[k]; P->gs[k] = nullptr; }
-      for (uint32_t k = 0; k < MAX_GROUPS; k++) { a.gev[k] = P->gev[k]; P->gev[k] = nullptr; }
-      aux_free().push_back(a);
+      aux_free().push_back(AuxSet{dev, P->aux, P->fork, P->join});
       P->aux = nullptr; P->fork = P->join = nullptr;
       return;
     }
@@ -922,11 +839,7 @@ void aux_give(zd_plan* P) {
   if (P->fork) (void)hipEventDestroy(P->fork);
   if (P->join) (void)hipEventDestroy(P->join);
   if (P->aux) (void)hipStreamDestroy(P->aux);
-  for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) if (P->gs[k]) (void)hipStreamDestroy(P->gs[k]);
-  for (uint32_t k = 0; k < MAX_GROUPS; k++) if (P->gev[k]) (void)hipEventDestroy(P->gev[k]);
   P->aux = nullptr; P->fork = P->join = nullptr;
-  for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) P->gs[k] = nullptr;
-  for (uint32_t k = 0; k < MAX_GROUPS; k++) P->gev[k] = nullptr;
 }
 
 // Frames from in (FrameIterator::next, frame.rs:94-99) into `part` until the
@@ -1560,7 +1473,6 @@ void zd_plan_destroy(zd_plan* P) {
   if (P->launched) {
     (void)hipStreamSynchronize(P->last_stream);
     if (P->aux) (void)hipStreamSynchronize(P->aux);
-    for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) if (P->gs[k]) (void)hipStreamSynchronize(P->gs[k]);
   }
   ws_release(P->d_ws, P->ws_bytes, P->dev);
   if (P->d_staging) (void)hipFree(P->d_staging);
@@ -1646,12 +1558,6 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   static const char* fork_env = getenv("ZD_FORK");
   const bool fork = fork_env ? atoi(fork_env) == 1 : fork_auto(P->n_seq);
   if (fork) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
-  if (P->n_groups > 1 && P->gs[P->n_groups - 2]) {
-    a.n_groups = P->n_groups;
-    for (uint32_t g = 0; g <= P->n_groups; g++) { a.g_seq[g] = P->g_seq[g]; a.g_k4[g] = P->g_k4[g]; a.g_k4f[g] = P->g_k4f[g]; }
-    for (uint32_t k = 0; k + 1 < MAX_GROUPS; k++) a.gs[k] = P->gs[k];
-    for (uint32_t k = 0; k < MAX_GROUPS; k++) a.gev[k] = P->gev[k];
-  }
   HIPCHK(launch_pipeline(a));
   P->launched = true;
   P->last_stream = s;
@@ -1707,11 +1613,14 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
   if (need_compact && !from.empty()) {
     // exact layout but a frame came out shorter than its FCS: move through a staging copy
     const uint8_t* stage = P->d_staging;
-    uint8_t* tmp = nullptr;
     if (P->info.out_exact) {
-      HIPCHK(hipMalloc(&tmp, std::max<uint64_t>(P->info.out_bytes, 16)));
-      HIPCHK(hipMemcpyAsync(tmp, d_dst, P->info.out_bytes, hipMemcpyDeviceToDevice, s));
-      stage = tmp;
+      // the plan's staging buffer, made on the first such call and kept
+      if (!P->d_staging) {
+        P->staging_bytes = P->info.out_bytes;
+        HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
+      }
+      HIPCHK(hipMemcpyAsync(P->d_staging, d_dst, P->info.out_bytes, hipMemcpyDeviceToDevice, s));
+      stage = P->d_staging;
     }
     size_t m = from.size();
     if (!grow_dev(P->d_meta, P->meta_cap, 3 * m)) return ZD_E_HIP;
@@ -1721,7 +1630,6 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
     HIPCHK(hipMemcpy(d_meta + 2 * m, len.data(), m * 8, hipMemcpyHostToDevice));
     HIPCHK(launch_compact(stage, d_dst, d_meta, d_meta + m, d_meta + 2 * m, (uint32_t)m, s));
     HIPCHK(hipStreamSynchronize(s));
-    if (tmp) (void)hipFree(tmp);
   }
   if (first < 0 && P->index_status) { first = (int)nf; overall = P->index_status; }
   P->res_off = to;

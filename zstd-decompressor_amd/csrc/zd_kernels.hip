@@ -152,9 +152,6 @@ constexpr int K1_BIG = 1;
 // the reference keeps every weight, its symbols wrapping as u8
 // (huffman.rs:161-175); the block goes to the third pass (zd_k_tables_huge).
 constexpr int K1_HUGE = 2;
-// Three lanes per block (zd_k_tables_seq3): an earlier table failed to parse;
-// the lane building that table reports it.
-constexpr int K1_DEFER = 3;
 constexpr uint32_t K1S_SYMS = 64;
 
 // parse_fse_table (fse.rs:16-69); dist holds max_sym entries (256: all)
@@ -519,21 +516,18 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
 // descriptions and predefined distributions, in LL, OF, ML order, each
 // written as compact entries to the block's slot.  Returns status; *stage_sub
 // = table index of a failure (3: the empty-bitstream check).
-// only: build table `only` alone (0 LL, 1 OF, 2 ML; the headers before it are
-// parsed to find it, and table 2's lane finds the bitstream), -1: all three.
 template <typename LN>
 __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, LN& L, uint16_t* slot, uint8_t al_out[3],
-                                 uint32_t* bs_off, uint32_t* bs_size, int* sub, int only = -1) {
+                                 uint32_t* bs_off, uint32_t* bs_size, int* sub) {
   uint32_t pos = C.seq_tables;
   for (int k = 0; k < 3; k++) {
     *sub = k;
     const int mode = C.modes[k];
-    const bool build = only < 0 || only == k;
     uint16_t* tab = slot + k * FSE_TAB;
     int st = 0, al = 0;
     if (mode == M_RLE) {
       if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
-      else { if (build) tab[0] = fse_entry(blk[pos], 1); pos++; }   // AL 0: nb 0, baseline 0
+      else { tab[0] = fse_entry(blk[pos], 1); pos++; }   // AL 0: nb 0, baseline 0
     } else if (mode == M_FSE) {
       if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
       else {
@@ -541,7 +535,7 @@ __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, LN& L, 
         uint8_t a;
         uint32_t nsym;
         st = parse_ncount(fw, &a, L.dist, &nsym, LN::SYMS);
-        if (!st && build) st = build_fse(a, L.dist, nsym, tab, L.sym, L.next);
+        if (!st) st = build_fse(a, L.dist, nsym, tab, L.sym, L.next);
         al = a;
         pos += fw.bytes_read();
       }
@@ -549,14 +543,11 @@ __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, LN& L, 
       const int16_t* d = k == 0 ? c_ll_default : (k == 1 ? c_of_default : c_ml_default);
       const uint32_t nsym = k == 0 ? 36 : (k == 1 ? 29 : 53);
       al = k == 1 ? 5 : 6;
-      if (build) {
-        for (uint32_t x = 0; x < nsym; x++) L.dist[x] = d[x];
-        st = build_fse(al, L.dist, nsym, tab, L.sym, L.next);
-      }
+      for (uint32_t x = 0; x < nsym; x++) L.dist[x] = d[x];
+      st = build_fse(al, L.dist, nsym, tab, L.sym, L.next);
     }
-    if (st) return (only >= 0 && k < only && st != K1_BIG) ? K1_DEFER : st;
+    if (st) return st;
     if (mode != M_REPEAT) al_out[k] = (uint8_t)al;
-    if (only >= 0 && only == k && k < 2) return 0;
   }
   *sub = 3;
   *bs_off = pos;                                  // seq.bitstream = input.slice(input.len()) (sequences.rs:72)
@@ -626,43 +617,6 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
     cstate[ci].bs_size = bsz;
     if (st) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, (uint32_t)sub, st));
   }
-}
-
-// K1's sequence half for plans of few blocks (the few-frames regime, where
-// K1 is one round of serial per-lane builds on K3's critical path): three
-// lanes per block, lane k builds table k (C3: one table per lane instead of
-// three).  Same tables, CompState bytes and error keys as zd_k_tables<false,
-// 2>; blocks with a table of more than 64 symbols go to its large pass.
-constexpr int K1Q_BLOCKS = 16;
-__global__ __launch_bounds__(3 * K1Q_BLOCKS) void zd_k_tables_seq3(const uint8_t* __restrict__ src,
-                                                                    const CompBlock* __restrict__ comp,
-                                                                    CompState* cstate, FrameState* fstate,
-                                                                    const uint32_t* __restrict__ list,
-                                                                    uint32_t n_list, uint16_t* fses) {
-  __shared__ K1LaneS lanes[3 * K1Q_BLOCKS];
-  const uint32_t t = threadIdx.x, k = t % 3;
-  const uint32_t li = blockIdx.x * K1Q_BLOCKS + t / 3;
-  if (li >= n_list) return;
-  K1LaneS& L = lanes[t];
-  const uint32_t ci = list[li];
-  const CompBlock C = comp[ci];
-  if (C.prebuilt || !(C.nseq > 0 && C.host_stage > PS_SEQ_TABLES)) return;
-  uint8_t al[3] = {0, 0, 0};
-  uint32_t bo = 0, bsz = 0;
-  int sub = 0;
-  const int st = k1_sequences_lane(src + C.src, C, L, fses + (uint64_t)C.fse_slot * FSE_SLOT, al, &bo, &bsz, &sub,
-                                   (int)k);
-  if (st == K1_BIG) {
-    cstate[ci].k1_bigs = 1;
-    return;
-  }
-  if (st == K1_DEFER) return;
-  if (C.modes[k] != M_REPEAT && (sub > (int)k || !st)) cstate[ci].al[k] = al[k];
-  if (k == 2) {
-    cstate[ci].bs_off = bo;
-    cstate[ci].bs_size = bsz;
-  }
-  if (st) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, (uint32_t)sub, st));
 }
 
 // Trees whose weight stream runs past 255 weights (non-conforming input):
@@ -812,14 +766,11 @@ struct WinU {
 };
 typedef uint64_t u64x2a1 __attribute__((ext_vector_type(2), aligned(1)));
 typedef __attribute__((address_space(1))) const u64x2a1 g_u64x2a1;
-template <bool NT = false>
 __device__ inline WinU winu_load(const uint8_t* s, uintptr_t base, int32_t pos) {
   const int32_t tb = (pos + 7) >> 3;
   uintptr_t a = (uintptr_t)((intptr_t)s + tb - 16);
   a = a < base ? base : a;
-  u64x2a1 v;
-  if constexpr (NT) v = __builtin_nontemporal_load((g_u64x2a1*)a);
-  else v = *(g_u64x2a1*)a;
+  const u64x2a1 v = *(g_u64x2a1*)a;
   WinU w;
   w.w0 = v.x;
   w.w1 = v.y;
@@ -1792,15 +1743,8 @@ __device__ inline uint64_t rec_lane(uint64_t raw, int lane) {
 #endif
 constexpr int K4_W = ZD_K4_W;                 // history kept after a slide
 constexpr int K4_B = ZD_K4_B;                 // room kept for a batch (a slide when less is left)
-#ifndef ZD_K4_STSB
-#define ZD_K4_STSB 0                  // branchless partial stores in the batch loop (sts_nb)
-#endif
 #ifndef ZD_K4_C
-#if ZD_K4_STSB
-#define ZD_K4_C 7088                  // (room for the 512-byte dump slots: 16 waves per CU)
-#else
 #define ZD_K4_C 7200
-#endif
 #endif
 constexpr int K4_C = ZD_K4_C;                 // window bytes
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -1816,19 +1760,14 @@ typedef __attribute__((address_space(3))) u32x4 l_u32x4;
 
 __device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
 // Match sources in HBM are read through the caches: the frame's own recent
-// output, re-read by later matches (nontemporal loads here: 28.3 -> 23.4 ms)
-__device__ inline u32x4 ldg16_nt(const uint8_t* p) { return *(g_cu32x4a1*)p; }
-// streams read once (records, literals): nontemporal, to leave the caches
-// to the frame outputs
-#ifndef ZD_K4_NT
-#define ZD_K4_NT 0                    // read-once streams (records, windows, literal stage) nontemporal
-#endif
+// output, re-read by later matches (plain loads: the nontemporal form took
+// 28.3 ms against 23.4 in round 1)
+__device__ inline u32x4 ldg16_src(const uint8_t* p) { return *(g_cu32x4a1*)p; }
+// streams read once (records, literals): plain loads (nontemporal loads of
+// the records, windows and literal stage measured slower: 1 GiB K4 2.06 ->
+// 2.11 ms)
 __device__ inline u32x4 ldg16_once(const uint8_t* p) {
-#if ZD_K4_NT
-  return __builtin_nontemporal_load((g_cu32x4a1*)p);
-#else
   return *(g_cu32x4a1*)p;
-#endif
 }
 __device__ inline u32x4 lds16(const l_u8* p) { return *(const l_u32x4a1*)p; }
 // stores the first n (0..16) bytes of v at p
@@ -1838,19 +1777,6 @@ __device__ inline void sts_n(l_u8* p, u32x4 v, uint32_t n) {
   if (n & 4) { *(l_u32a1*)p = v.x; v.x = v.y; p += 4; }
   if (n & 2) { *(l_u16a1*)p = (uint16_t)v.x; v.x >>= 16; p += 2; }
   if (n & 1) { *p = (uint8_t)v.x; }
-}
-// sts_n without branches for n < 16: the 8 / 4 / 2 / 1-byte parts of n each
-// go to p or, when n lacks them, to this lane's 8-byte dump slot (no exec
-// mask juggling: four LDS stores and a few selects per piece)
-__device__ inline void sts_nb(l_u8* p, u32x4 v, uint32_t n, l_u8* dump) {
-  if (n >= 16) { *(l_u32x4a1*)p = v; return; }
-  const bool b8 = (n & 8) != 0, b4 = (n & 4) != 0, b2 = (n & 2) != 0, b1 = (n & 1) != 0;
-  *(l_u64a1*)(b8 ? p : dump) = (uint64_t)v.x | ((uint64_t)v.y << 32);
-  const uint32_t x0 = b8 ? v.z : v.x, x1 = b8 ? v.w : v.y;
-  *(l_u32a1*)(b4 ? p + (n & 8) : dump) = x0;
-  const uint32_t y = b4 ? x1 : x0;
-  *(l_u16a1*)(b2 ? p + (n & 12) : dump) = (uint16_t)y;
-  *(b1 ? p + (n & 14) : dump) = (uint8_t)(y >> ((n & 2) << 3));
 }
 __device__ inline void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // The smallest multiple of the period off (1..15) that is >= 16, without a
@@ -1918,7 +1844,7 @@ struct K4W {
   __device__ inline int32_t space() const { return C - (pos - hs); }
   __device__ inline int32_t alignd(int32_t p) const { return ((p - a0) & ~15) + a0; }
   // 16 bytes of frame output at p (p >= 0): LDS when inside the window, else HBM
-  __device__ inline u32x4 src16(int32_t p) const { return p >= hs ? lds16(at(p)) : ldg16_nt(out + (uint32_t)p); }
+  __device__ inline u32x4 src16(int32_t p) const { return p >= hs ? lds16(at(p)) : ldg16_src(out + (uint32_t)p); }
 };
 typedef K4W<K4_C, K4_W, K4_B> K4;
 
@@ -2078,19 +2004,12 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                                                    const uint8_t* __restrict__ lits,
                                                    const uint64_t* __restrict__ seqs,
                                                    const uint16_t* __restrict__ fses, uint32_t f_begin,
-                                                   uint32_t f_end, const uint32_t* __restrict__ flist) {
+                                                   uint32_t f_end) {
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
   __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
   const int lane = threadIdx.x;
-#if ZD_K4_STSB
-  __shared__ __attribute__((aligned(16))) uint8_t dumps[64 * 8];
-  l_u8* const dmp = (l_u8*)dumps + 8 * lane;
-#define STS(p, v, n) sts_nb(p, v, n, dmp)
-#else
-#define STS(p, v, n) sts_n(p, v, n)
-#endif
 #if ZD_K4_CODELUT
   // LL | ML code -> baseline | extra-bit count << 24 (ll_code / ml_code,
   // sequences.rs tables), one LDS read per code instead of ~20 VALU ops
@@ -2104,10 +2023,8 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     k4_sync();
   }
 #endif
-  // persistent over frames when the grid is capped; entries [f_begin, f_end)
-  // of flist (a chain group's frames) or frames f_begin .. f_end - 1
-  for (uint32_t fl_i = f_begin + blockIdx.x; fl_i < f_end; fl_i += gridDim.x) {
-  const uint32_t f = flist ? flist[fl_i] : fl_i;
+  // persistent over frames when the grid is capped
+  for (uint32_t f = f_begin + blockIdx.x; f < f_end; f += gridDim.x) {
   const FrameDesc F = frames[f];
   if (F.lds) continue;                           // K4F executes this frame
   FrameState* S = &fstate[f];
@@ -2192,14 +2109,10 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     // odd record runs that one sequence alone, so batches start even.  The
     // context API's direct records are one 8-byte word each.
     const uint32_t n_ld = direct ? n : (n + 1) & ~1u;
-#if ZD_K4_NT
-    auto rec_at = [&](uint32_t i) -> uint64_t { return i < n_ld ? __builtin_nontemporal_load(SQ + i) : 0; };
-#else
     auto rec_at = [&](uint32_t i) -> uint64_t { return i < n_ld ? SQ[i] : 0; };
-#endif
     auto rec_of = [&](uint64_t raw) -> uint64_t { return direct ? raw : rec_lane(raw, lane); };
     auto win_of = [&](uint64_t r, bool v) -> WinU {
-      return winu_load<ZD_K4_NT>(bsp, (uintptr_t)src, (v && !direct) ? (int32_t)(uint32_t)r : 0);
+      return winu_load(bsp, (uintptr_t)src, (v && !direct) ? (int32_t)(uint32_t)r : 0);
     };
     auto lit_of = [&](uint32_t cur) -> u32x4 {
       return (lit_stage && 16 * (uint32_t)lane < K4_STG && cur + 16 * (uint32_t)lane < nl) ? ldg16_once(lsrc + cur + 16 * lane) : f4;
@@ -2322,8 +2235,8 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                          shi <= (X.hs < fl_safe ? X.hs : fl_safe);
         u32x4 fv0, fv1;
         if (far) {
-          fv0 = ldg16_nt(X.out + (uint32_t)slo);
-          if (ml > 16) fv1 = ldg16_nt(X.out + (uint32_t)(slo + 16));
+          fv0 = ldg16_src(X.out + (uint32_t)slo);
+          if (ml > 16) fv1 = ldg16_src(X.out + (uint32_t)(slo + 16));
         }
         // matches whose source lies wholly in the window and before this
         // batch (written by earlier batches, so no order among the lanes):
@@ -2367,9 +2280,9 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           l_u8* d = X.at(X.pos + (int32_t)opos);
           if (!lit_stage || lpos + ll <= K4_STG) {
             const l_u8* sp = (const l_u8*)stg + lpos;
-            for (uint32_t x = 0; x < ll; x += 16) STS(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, lit_stage ? lds16(sp + x) : f4, ll - x);
           } else {
-            for (uint32_t x = 0; x < ll; x += 16) STS(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
           }
         }
         K4_PHASE(2);
@@ -2379,11 +2292,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           l_u8* d = X.at(q);
           u32x4 a0 = fv0;
           if (inwin) a0 = lds16(X.at(slo));
-          STS(d, a0, ml);
+          sts_n(d, a0, ml);
           if (ml > 16) {
             u32x4 a1 = fv1;
             if (inwin) a1 = lds16(X.at(slo + 16));
-            STS(d + 16, a1, ml - 16);
+            sts_n(d + 16, a1, ml - 16);
           }
           // the rest four pieces at a time: one load latency per 64 bytes
           for (uint32_t x = 32; x < ml; x += 64) {
@@ -2395,15 +2308,15 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
               if (x + 48 < ml) v3 = lds16(X.at(slo + (int32_t)x + 48));
             } else {
               const uint8_t* sp = X.out + (uint32_t)slo;
-              v0 = ldg16_nt(sp + x);
-              if (x + 16 < ml) v1 = ldg16_nt(sp + x + 16);
-              if (x + 32 < ml) v2 = ldg16_nt(sp + x + 32);
-              if (x + 48 < ml) v3 = ldg16_nt(sp + x + 48);
+              v0 = ldg16_src(sp + x);
+              if (x + 16 < ml) v1 = ldg16_src(sp + x + 16);
+              if (x + 32 < ml) v2 = ldg16_src(sp + x + 32);
+              if (x + 48 < ml) v3 = ldg16_src(sp + x + 48);
             }
-            STS(d + x, v0, ml - x);
-            if (x + 16 < ml) STS(d + x + 16, v1, ml - x - 16);
-            if (x + 32 < ml) STS(d + x + 32, v2, ml - x - 32);
-            if (x + 48 < ml) STS(d + x + 48, v3, ml - x - 48);
+            sts_n(d + x, v0, ml - x);
+            if (x + 16 < ml) sts_n(d + x + 16, v1, ml - x - 16);
+            if (x + 32 < ml) sts_n(d + x + 32, v2, ml - x - 32);
+            if (x + 48 < ml) sts_n(d + x + 48, v3, ml - x - 48);
           }
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
@@ -2417,7 +2330,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
           if (mine) {
             l_u8* d = X.at(q);
             if (off32 >= 16) {
-              for (uint32_t x = 0; x < ml; x += 16) STS(d + x, X.src16(slo + (int32_t)x), ml - x);
+              for (uint32_t x = 0; x < ml; x += 16) sts_n(d + x, X.src16(slo + (int32_t)x), ml - x);
             } else {                             // small period: first 16 bytes bytewise, then 16-byte steps
               const uint32_t m16 = period16(off32);
               const uint32_t head = ml < 16 ? ml : 16;
@@ -2426,7 +2339,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                 d[x] = *X.at(slo + (int32_t)r);
                 r = r + 1 == off32 ? 0 : r + 1;
               }
-              for (uint32_t x = 16; x < ml; x += 16) STS(d + x, lds16(d + x - m16), ml - x);
+              for (uint32_t x = 16; x < ml; x += 16) sts_n(d + x, lds16(d + x - m16), ml - x);
             }
           }
           done |= __ballot(mine);
@@ -3579,13 +3492,6 @@ __global__ __launch_bounds__(256) void zd_k_compact(const uint8_t* __restrict__ 
 // ---------------------------------------------------------------------------
 // launch
 // ---------------------------------------------------------------------------
-// K1's sequence half three lanes per block up to this many blocks with tables
-// (a few-frames plan: one round of per-lane builds)
-#ifndef ZD_K1Q_MAX
-#define ZD_K1Q_MAX 16384
-#endif
-constexpr uint32_t K1Q_MAX_TABLES = ZD_K1Q_MAX;
-
 hipError_t launch_pipeline(const LaunchArgs& a) {
   uint8_t* ws = a.ws;
   const Workspace& W = a.W;
@@ -3628,15 +3534,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (a.n_tables) {
     if (fork) {
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
-      if (a.n_tables <= K1Q_MAX_TABLES) {
-        const uint32_t* lt = (const uint32_t*)(ws + W.list_tables);
-        hipLaunchKernelGGL(zd_k_tables_seq3, dim3((a.n_tables + K1Q_BLOCKS - 1) / K1Q_BLOCKS), dim3(3 * K1Q_BLOCKS),
-                           0, s, a.src, comp, cstate, fstate, lt, a.n_tables, fses);
-        hipLaunchKernelGGL((zd_k_tables<true, 2>), dim3((a.n_tables + K1_LANES - 1) / K1_LANES), dim3(K1_LANES), 0, s,
-                           a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses, huge);
-      } else {
-        k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
-      }
+      k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
     } else {
       k1(zd_k_tables<false, 3>, zd_k_tables<true, 3>, s, true);
     }
@@ -3658,13 +3556,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                            cstate, fstate, list, n, (const uint16_t*)fses, seqs);
     }
   };
-  // frames [f0, f1) of the plan, or entries [f0, f1) of flist
-  auto k4 = [&](uint32_t f0, uint32_t f1, const uint32_t* flist, hipStream_t st) {
+  auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st) {
     const uint32_t n = f1 - f0;
     if (n && a.n_frames > a.n_k4f)   // frames on the streaming K4 (K4F's exit at once)
       hipLaunchKernelGGL(zd_k_execute, dim3(n),
                          dim3(64), 0, st, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
-                         (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1, flist);
+                         (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1);
   };
   auto k4f = [&](const uint32_t* list, uint32_t n, hipStream_t st) {
     if (n)
@@ -3672,34 +3569,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                          (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                          (const uint16_t*)fses, list);
   };
-  if (a.n_groups > 1 && !a.events) {
-    // chain groups: group g's K3, then (K2 done) its K4 / K4F, on stream g
-    const uint32_t* lsg = (const uint32_t*)(ws + W.list_seq_g);
-    const uint32_t* lk4 = (const uint32_t*)(ws + W.list_k4_g);
-    const uint32_t* lkf = (const uint32_t*)(ws + W.list_k4f_g);
-    if ((e = hipEventRecord(a.gev[0], s)) != hipSuccess) return e;
-    for (uint32_t g = 0; g < a.n_groups; g++) {
-      hipStream_t st = g ? a.gs[g - 1] : s;
-      if (g)
-        if ((e = hipStreamWaitEvent(st, a.gev[0], 0)) != hipSuccess) return e;
-      k3(lsg + a.g_seq[g], a.g_seq[g + 1] - a.g_seq[g], st);
-      if (fork)
-        if ((e = hipStreamWaitEvent(st, a.join, 0)) != hipSuccess) return e;
-      k4(a.g_k4[g], a.g_k4[g + 1], lk4, st);
-      k4f(lkf + a.g_k4f[g], a.g_k4f[g + 1] - a.g_k4f[g], st);
-    }
-    for (uint32_t g = 1; g < a.n_groups; g++) {
-      if ((e = hipEventRecord(a.gev[g], a.gs[g - 1])) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(s, a.gev[g], 0)) != hipSuccess) return e;
-    }
-  } else {
-    k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s);
-    if (fork)
-      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-    if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
-    k4(0, a.n_frames, nullptr, s);
-    k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s);
-  }
+  k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s);
+  if (fork)
+    if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
+  if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
+  k4(0, a.n_frames, s);
+  k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s);
   if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;
   if (a.n_jframes) {
     auto* jframes = (const JFrame*)(ws + W.jframes);

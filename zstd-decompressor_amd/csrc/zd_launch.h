@@ -7,8 +7,6 @@
 
 namespace zd {
 
-constexpr uint32_t MAX_GROUPS = 3;         // chain groups: 3 + the K2 stream = the process's 4 HW queues
-
 struct LaunchArgs {
   const uint8_t* src;      // d_src
   uint64_t src_size;
@@ -25,14 +23,6 @@ struct LaunchArgs {
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
   bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block
   uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
-  // Chain groups (plans whose K3 chains fit one round): group g's K3 and then
-  // its K4 / K4F run on their own stream, so the frames of short chains
-  // execute while longer chains still run.  Group g holds entries
-  // [g_x[g], g_x[g + 1]) of the grouped lists (Workspace list_*_g).
-  uint32_t n_groups = 0;
-  uint32_t g_seq[MAX_GROUPS + 1] = {}, g_k4[MAX_GROUPS + 1] = {}, g_k4f[MAX_GROUPS + 1] = {};
-  hipStream_t gs[MAX_GROUPS - 1] = {};     // streams of groups 1 .. n_groups - 1 (group 0 on `stream`)
-  hipEvent_t gev[MAX_GROUPS] = {};         // [0]: tables built; [g]: group g done
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
