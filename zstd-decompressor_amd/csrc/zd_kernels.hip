@@ -207,7 +207,8 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
 // a 16-bit entry (zd_common.h fse_entry); nbits/baseline follow from it and
 // equal the reference's parts/base_width construction (fse.rs:169-189).
 // `-1` symbols count as 1.  sym/next are LDS scratch (T and 256 entries).
-__device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* table, uint8_t* sym, uint16_t* next) {
+__device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* __restrict__ table, uint8_t* sym,
+                         uint16_t* next) {
   if (al > FSE_MAX_AL) return ZD_E_LARGE_ACCURACY_LOG;
   uint32_t T = 1u << al;
   uint32_t zero_pos = T;
@@ -219,13 +220,16 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* t
   }
   uint32_t pos = 0, step = (T >> 1) + (T >> 3) + 3, mask = T - 1, placed = 0;
   for (uint32_t s = 0; s < nsym; s++) {
-    for (int k = 0; k < dist[s]; k++) {
-      if (zero_pos == 0) return ZD_E_REF_PANIC;   // the reference loops forever
+    // the count in a register: sym (bytes) may alias dist for the compiler,
+    // which would reload it from LDS on every placement
+    const int c = dist[s];
+    if (c > 0 && zero_pos == 0) return ZD_E_REF_PANIC;   // the reference loops forever
+    for (int k = 0; k < c; k++) {
       sym[pos] = (uint8_t)s;
-      placed++;
       pos = (pos + step) & mask;
       while (pos >= zero_pos) pos = (pos + step) & mask;
     }
+    placed += c > 0 ? (uint32_t)c : 0u;
   }
   if (placed != zero_pos) return ZD_E_CORRUPTED_TABLE;
   for (uint32_t s = 0; s < nsym; s++) next[s] = dist[s] > 0 ? (uint16_t)dist[s] : (dist[s] == -1 ? 1 : 0);
@@ -300,7 +304,7 @@ __device__ inline uint32_t lut_width(uint32_t e, bool s32) {
 // (the entries just outside hold codes or lie past the table), which is the
 // number of bits HuffmanDecoder::decode (huffman.rs:205-218) reads before
 // it hits the node and panics.
-__device__ void lut_holes(uint16_t* lut, int p, uint32_t a, uint32_t b) {
+__device__ void lut_holes(uint16_t* __restrict__ lut, int p, uint32_t a, uint32_t b) {
   for (uint32_t e = a; e < b; e++) {
     int k = p;
     for (; k > 0; k--) {
@@ -414,7 +418,7 @@ __device__ int k1_weight_stream(const uint8_t* desc, const uint8_t* src, const u
 // a tree of 256 symbols) returns K1_HUGE: the third pass takes the block.
 template <typename LN>
 __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, LN& L,
-                               uint16_t* lut, int* p_out) {
+                               uint16_t* __restrict__ lut, int* p_out) {
   int st = 0;
   uint32_t nw = 0;
   const uint8_t h = desc[0];
