@@ -207,9 +207,18 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
 // a 16-bit entry (zd_common.h fse_entry); nbits/baseline follow from it and
 // equal the reference's parts/base_width construction (fse.rs:169-189).
 // `-1` symbols count as 1.  sym/next are LDS scratch (T and 256 entries).
+#ifdef ZD_K1_PROF
+__device__ uint64_t k1_prof[8];
+#define K1T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define K1ADD(i, a, b) atomicAdd((unsigned long long*)&k1_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define K1T(v) do { } while (0)
+#define K1ADD(i, a, b) do { } while (0)
+#endif
 __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* __restrict__ table, uint8_t* sym,
                          uint16_t* next) {
   if (al > FSE_MAX_AL) return ZD_E_LARGE_ACCURACY_LOG;
+  K1T(t0);
   uint32_t T = 1u << al;
   uint32_t zero_pos = T;
   for (uint32_t s = 0; s < nsym; s++) {
@@ -232,6 +241,8 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* _
     placed += c > 0 ? (uint32_t)c : 0u;
   }
   if (placed != zero_pos) return ZD_E_CORRUPTED_TABLE;
+  K1T(t1);
+  K1ADD(0, t0, t1);
   for (uint32_t s = 0; s < nsym; s++) next[s] = dist[s] > 0 ? (uint16_t)dist[s] : (dist[s] == -1 ? 1 : 0);
   // next[s]++ in state order, four states a step (T >= 32): one LDS round
   // trip for the four counters instead of one per state; a symbol met again
@@ -254,6 +265,8 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* _
     table[i + 2] = fse_entry(s2, t2);
     table[i + 3] = fse_entry(s3, t3);
   }
+  K1T(t2);
+  K1ADD(1, t1, t2);
   return 0;
 }
 
@@ -422,6 +435,7 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
   int st = 0;
   uint32_t nw = 0;
   const uint8_t h = desc[0];
+  K1T(h0);
   if (h < 128) {
     st = k1_weight_stream(desc, src, src_end, L, [&](uint32_t i, uint32_t w) {
       if (i >= K1_MAX_WEIGHTS) return false;
@@ -437,6 +451,8 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
     }
   }
   if (st) return st;
+  K1T(h1);
+  K1ADD(3, h0, h1);
   // from_weights (huffman.rs:177-203)
   uint32_t sum = 0;
   for (uint32_t i = 0; i < nw; i++) {
@@ -496,6 +512,8 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
     pos = al + k * S;
   }
   lut_holes(lut, p, pos, T);
+  K1T(h2);
+  K1ADD(4, h1, h2);
   for (int w = 0; w <= p; w++) L.cnt[w] = 0;  // reused as rank counters
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t wt = L.weights[i];
@@ -513,6 +531,8 @@ __device__ int k1_huffman_lane(const uint8_t* desc, const uint8_t* src, const ui
       for (uint32_t e = 0; e < S; e++) lut[at + e] = ent;
     }
   }
+  K1T(h3);
+  K1ADD(5, h2, h3);
   *p_out = p;
   return 0;
 }
@@ -538,7 +558,10 @@ __device__ int k1_sequences_lane(const uint8_t* blk, const CompBlock& C, LN& L, 
         FwBits fw{blk + pos, C.size - pos, 0};
         uint8_t a;
         uint32_t nsym;
+        K1T(p0);
         st = parse_ncount(fw, &a, L.dist, &nsym, LN::SYMS);
+        K1T(p1);
+        K1ADD(2, p0, p1);
         if (!st) st = build_fse(a, L.dist, nsym, tab, L.sym, L.next);
         al = a;
         pos += fw.bytes_read();
@@ -576,6 +599,10 @@ __global__ __launch_bounds__(K1_LANES) void zd_k_tables(const uint8_t* __restric
   __shared__ LN lanes[K1_LANES];
   const uint32_t li = blockIdx.x * K1_LANES + threadIdx.x;
   if (li >= n_list) return;
+  K1T(k0);
+#ifdef ZD_K1_PROF
+  struct Done { uint64_t t; __device__ ~Done() { K1T(k1); K1ADD(6, t, k1); atomicAdd((unsigned long long*)&k1_prof[7], 1ull); } } done_{k0};
+#endif
   LN& L = lanes[threadIdx.x];
   const uint32_t ci = list[li];
   if (BIG && !(((PART & 1) && cstate[ci].k1_bigh) || ((PART & 2) && cstate[ci].k1_bigs))) return;
@@ -3604,6 +3631,18 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   return hipGetLastError();
 }
 
+#ifdef ZD_K1_PROF
+}  // namespace zd
+extern "C" int zd_debug_k1_prof(uint64_t out[8], int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zd::k1_prof), 64, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (reset) {
+    static const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(zd::k1_prof), z, 64, 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  }
+  return 0;
+}
+namespace zd {
+#endif
 hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* d_from, const uint64_t* d_to,
                           const uint64_t* d_len, uint32_t n, hipStream_t s) {
   if (!n) return hipSuccess;
