@@ -151,6 +151,10 @@ typedef struct zd_plan zd_plan;
 /* Sequence-decode choice: K3 with one lane per block instead of four (the
  * default, K3Q).  Same records either way; tests run both. */
 #define ZD_F_SEQ_ONE_LANE   8u
+/* Launch choice for plans of 256-1024 single-block frames:
+ * K3 and K4 run fused per frame group (zd_k_fused) by default; this flag
+ * keeps them as two launches.  Same output either way; tests run both. */
+#define ZD_F_NO_FUSE      32u
 
 typedef struct zd_plan_info {
   uint64_t nframes;        /* frames in the plan (skippable included) */

@@ -300,6 +300,47 @@ def test_mixed_frame_plans():
             assert_parity(bytes(d), False, f"{name} corrupt #{it}")
 
 
+def test_fused_plans():
+    """Plans of 256-1024 single-block frames run K3 and K4 fused per group of
+    four frames (zd_k_fused: the K4 waves follow their chains' published
+    records; a chain the fast path rejects goes to the redo pass);
+    ZD_F_NO_FUSE keeps two launches.  Both against the oracle: 300 frames of
+    2-128 KiB at levels 1/3/9/19 (raw, RLE and Huffman literals, repeat
+    offsets), a C3-shaped plan of 400 x 128 KiB, and corruptions inside both
+    (chains rejected mid-plan, K2 and K1 errors)."""
+    from zstd_decompressor import _lib
+    r = random.Random(91)
+    frames = []
+    for i in range(300):
+        n = r.choice([2048, 16384, 65536, 128 << 10])
+        kind = r.choice([gen.text, gen.text, gen.xml, gen.binary])
+        frames.append(gen.frames(kind(n, seed=3000 + i), 1 << 20, r.choice([1, 3, 9, 19])))
+    mixed = b"".join(frames)
+    c3 = gen.frames(gen.text(400 << 17, seed=23), 128 << 10, 3)
+    # the fused plan's layout on the two-launch pipeline too (the profiled
+    # path runs it): the host walk's parts must start on aligned slots
+    import torch
+    from zstd_decompressor.batch import Plan
+    plan = Plan(c3)
+    plan.set_profiling(True)
+    d_src = torch.frombuffer(bytearray(c3 + bytes(64)), dtype=torch.uint8).cuda()
+    d_dst = torch.zeros(plan.info.out_bytes + 64, dtype=torch.uint8, device="cuda")
+    plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), plan.info.out_bytes)
+    torch.cuda.synchronize()
+    st, total, _, _, _ = plan.results(d_dst.data_ptr())
+    ost, oout = oracle.decompress_status(c3)
+    assert (st, bytes(d_dst[:total].cpu().numpy())) == (ost, oout), "fused layout, profiled pipeline"
+    plan.close()
+    for flags in (_lib.F_NO_FUSE, 0):
+        for name, data in (("mixed", mixed), ("c3-shaped", c3)):
+            assert_parity(data, False, f"flags={flags} {name}", flags=flags)
+            for it in range(8):
+                d = bytearray(data)
+                for _ in range(r.randrange(1, 4)):
+                    d[r.randrange(len(d))] = r.randrange(256)
+                assert_parity(bytes(d), False, f"flags={flags} {name} corrupt #{it}", flags=flags)
+
+
 def test_plan_decompress_reuses_the_plan(resources):
     """zd_plan_decompress: host in / host out with a plan made once (the
     INTEGRATION.md decompress() pattern), equal to the oracle's output."""

@@ -73,6 +73,7 @@ struct zd_plan {
   // in the pinned staging until the upload: the vectors above stay empty)
   uint64_t n_comps = 0, n_blocks = 0, n_frames = 0, n_tables = 0, n_huf = 0, n_seq = 0, n_k4f = 0, n_copies = 0;
   uint64_t n_jframes = 0, n_jblk = 0, n_jseg = 0;
+  bool fused = false;                           // zd_k_fused plan (build_plan fuse_plan)
   std::vector<uint64_t> frame_out, frame_cap;   // output offset and capacity per frame
   bool staged = false;
   std::unique_lock<std::mutex> stage_lock;      // the pinned staging, from build_plan to upload_plan
@@ -172,6 +173,7 @@ struct PlanCtx {
   uint64_t rep0[3];
   uint32_t flags;
   bool k4f_on, k4j_auto;
+  bool fused;              // zd_k_fused plan: no K4F, 128-byte aligned literal and record slots
   int k4j_mode;
   uint32_t k4j_min;        // compressed blocks a frame needs for K4J (automatic mode)
 };
@@ -266,8 +268,9 @@ void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks,
           if (most > cb.lit_regen) cb.lit_extra = (uint32_t)(most - cb.lit_regen);
         }
         cb.lit_out = c.lits;
-        c.lits += align_up((uint64_t)cb.lit_regen + 24 + cb.lit_extra, 16);   // + K2's 8-byte slack
+        c.lits += align_up((uint64_t)cb.lit_regen + 24 + cb.lit_extra, X.fused ? 128 : 16);   // + K2's 8-byte slack
       }
+      if (X.fused) c.nrec = align_up(c.nrec, 16);   // a block's records start a 128-byte line
       cb.seq_out = c.nrec;
       c.nseq += cb.nseq;
       c.nrec += rec_slots(cb.nseq);              // record pairs, a spare pair past the block's last
@@ -481,6 +484,23 @@ size_t k3_slots() {
   return slots;
 }
 
+// zd_k_fused: K3 and K4 fused per group of four frames, for plans of few
+// single-block frames (the few-frames regime, C3: 763 frames).  Up to one
+// workgroup per CU, so K2's workgroups (which the fused K4 waves wait for)
+// always find room beside them.  ZD_FUSE=0/1 forces it off/on where allowed.
+constexpr size_t FUSE_MIN_FRAMES = 256;
+bool fuse_plan(const zd_plan* P, uint64_t out_len0) {
+  static const char* env = getenv("ZD_FUSE");
+  if (env && atoi(env) == 0) return false;
+  if ((P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) || out_len0) return false;
+  const size_t cus = k3_slots() / 64;
+  if (P->nframes < (env ? 1 : FUSE_MIN_FRAMES) || P->nframes > 4 * cus) return false;
+  for (const HostPart& hp : P->parts)
+    for (const HostFrame& hf : hp.frames)
+      if (hf.d.kind != ZD_FRAME_ZSTD || hf.key != KEY_NONE || hf.nb != 1) return false;
+  return true;
+}
+
 // Builds device-side descriptors from the host frames: one counting pass and
 // one filling pass over the parts in parallel (each part's entries start at
 // the counts of the parts before it), then the K4J descriptors in frame order.
@@ -500,6 +520,8 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   X.flags = P->flags;
   static const char* k4f_env = getenv("ZD_K4F");
   X.k4f_on = k4f_env ? atoi(k4f_env) == 1 : P->nframes >= K4F_AUTO_MIN_FRAMES && P->nframes <= K4F_AUTO_MAX_FRAMES;
+  X.fused = fuse_plan(P, out_len0);
+  if (X.fused) X.k4f_on = false;
   static const char* k4j_env = getenv("ZD_K4J");
   X.k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0 : (k4j_env ? atoi(k4j_env) : -1);
   X.k4j_min = P->nframes <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
@@ -516,6 +538,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     const HostPart& hp = P->parts[k];
     PlanCounts c;
     for (const HostFrame& hf : hp.frames) plan_frame<false>(X, hf, hp.blocks.data(), c, none, nullptr);
+    if (X.fused) {          // parts start aligned, so the filling pass pads exactly as this count did
+      c.lits = align_up(c.lits, 128);
+      c.nrec = align_up(c.nrec, 16);
+    }
     cnt[k + 1] = c;
   });
   for (size_t k = 1; k <= np; k++) { PlanCounts t = cnt[k - 1]; t.add(cnt[k]); cnt[k] = t; }
@@ -543,6 +569,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   P->n_comps = T.comps; P->n_blocks = T.blocks; P->n_frames = T.frames;
   P->n_tables = T.tables; P->n_huf = T.huf; P->n_seq = T.seq; P->n_k4f = T.k4f; P->n_copies = T.copies;
   P->n_jframes = T.jframes; P->n_jblk = T.jblk; P->n_jseg = T.jseg;
+  P->fused = X.fused && T.jframes == 0 && T.k4f == 0;
   P->frame_out.resize(T.frames);
   P->frame_cap.resize(T.frames);
   Sink S{};
@@ -652,6 +679,8 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
   W.jdone = carve(std::max<uint64_t>(j_pieces, 1));
   W.jst = carve(4 * P->j_bytes + 64);
+  W.redo = carve(std::max<uint64_t>(T.frames, 1));
+  W.k2done = carve(4);
   W.total = o;
 
   zd_plan_info& I = P->info;
@@ -1558,6 +1587,11 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   static const char* fork_env = getenv("ZD_FORK");
   const bool fork = fork_env ? atoi(fork_env) == 1 : fork_auto(P->n_seq);
   if (fork) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
+  if (P->fused && !P->profile) {
+    a.fused = true;
+    HIPCHK(hipMemsetAsync(P->d_ws + P->W.redo, 0, std::max<uint64_t>(P->n_frames, 1), s));
+    HIPCHK(hipMemsetAsync(P->d_ws + P->W.k2done, 0, 4, s));
+  }
   HIPCHK(launch_pipeline(a));
   P->launched = true;
   P->last_stream = s;

@@ -277,7 +277,10 @@ __device__ int build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* _
 // chip build tables at once.  Each lane keeps its scratch in LDS and writes
 // its Huffman LUT and compact FSE tables straight to the block's HBM slots.
 // ---------------------------------------------------------------------------
-constexpr int K1_LANES = 16;
+#ifndef ZD_K1_LANES
+#define ZD_K1_LANES 16
+#endif
+constexpr int K1_LANES = ZD_K1_LANES;
 constexpr int K1_MAX_WEIGHTS = 255;               // a Huffman tree of 256 symbols (RFC 8878 4.2.1)
 struct K1Lane {
   static constexpr uint32_t SYMS = 256, WFSE = FSE_TAB;
@@ -1074,7 +1077,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
                                                          const CompBlock* __restrict__ comp, CompState* cstate,
                                                          FrameState* fstate, const uint32_t* __restrict__ list,
                                                          uint32_t n_list, const uint16_t* __restrict__ luts,
-                                                         uint8_t* lits) {
+                                                         uint8_t* lits, uint32_t* k2done) {
   __shared__ __attribute__((aligned(16))) uint16_t lut[K2_BLOCKS][1 << K2_LUT_BITS];
   __shared__ uint32_t counts[K2_BLOCKS][4];
   __shared__ int errs[K2_BLOCKS][4];
@@ -1180,6 +1183,12 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     else
       (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)src, (g_u16*)g, p,
                                lits + C.lit_out + at, counts[b][k], &count, lits + C.lit_out + R + 16 + C.lit_extra);
+  }
+  // zd_k_fused's K4 waves wait for every K2 workgroup: the workgroup (one
+  // wave) releases its literals and CompState bytes at agent scope, then counts
+  if (k2done) {
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(k2done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1569,9 +1578,14 @@ __device__ inline uint32_t quad_max(uint32_t x) {
   x = max(x, qdpp<QP_SWAP1>(x));
   return max(x, qdpp<QP_SWAP2>(x));
 }
-template <int L, int N>
+// PUB (zd_k_fused): every 16 records the chain publishes to *prog the
+// 16-record lines of `out` whose stores have completed (a line eight pairs
+// back: vmcnt(32) leaves the newer window loads and stores in flight), for
+// the K4 wave of its workgroup.
+template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
-                          int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out) {
+                          int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
+                          volatile __attribute__((address_space(3))) uint32_t* prog = nullptr) {
   constexpr int U = (L % 2 == 0) ? L : 2 * L;
   if (bs_size == 0) return 1;
   const uint8_t lastb = bs[bs_size - 1];
@@ -1646,6 +1660,12 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
       asm volatile("" ::: "memory");
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
       outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
+      if constexpr (PUB) {
+        if (((slot + 2) & 15) == 0 && slot + 2 >= 32) {
+          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+          if (role == 0) *prog = (slot + 2 - 16) >> 4;
+        }
+      }
       step(w[(k + 1) % L]);
       pS = s;
       pPos = (uint32_t)pos;
@@ -1669,7 +1689,7 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
                                                        const CompBlock* __restrict__ comp, CompState* cstate,
                                                        FrameState* fstate, const uint32_t* __restrict__ list,
                                                        uint32_t n_list, const uint16_t* __restrict__ fses,
-                                                       uint64_t* __restrict__ recs) {
+                                                       uint64_t* __restrict__ recs, const uint8_t* __restrict__ redo) {
   __shared__ __attribute__((aligned(16))) uint16_t tabs[K3Q_CHAINS * K3_TAB];
   const int lane = threadIdx.x;
   const int role = lane & 3, q = lane >> 2;
@@ -1678,6 +1698,7 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
   const uint32_t ci = act ? list[li] : 0;
   CompBlock C;
   if (act) C = comp[ci];
+  if (act && redo && !redo[C.frame]) act = false;   // the redo pass after zd_k_fused: flagged frames only
   if (act) {
     const uint64_t key0 = fstate[C.frame].key;
     if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) act = false;
@@ -2027,7 +2048,54 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 #define ZD_K4_STG 512                       // C4, 4 GiB: 1024 8.36 ms, 512 8.25, 256 8.24
 #endif
 constexpr uint32_t K4_STG = ZD_K4_STG;      // literal bytes staged per batch (64 lanes x 16 at most)
-__global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __restrict__ src, uint8_t* outbase,
+typedef __attribute__((address_space(3))) uint32_t l_u32;
+// One K4 wave's LDS: the window, the period pattern, the block's LL | OF | ML
+// symbols, the batch's literal stage and the code tables.
+struct K4Lds {
+  l_u8* win;                 // K4_C bytes
+  l_u8* pat;                 // 64
+  l_u8* stab;                // 3 x FSE_TAB
+  l_u8* stg;                 // K4_STG + 16
+  l_u32* codelut;            // 2 x 64
+};
+// Fused mode (zd_k_fused): the frame's records arrive while K3 runs in the
+// same workgroup.  prog counts the 16-record lines K3 has completed
+// (K4F_PROG_FINAL: all, K4F_PROG_ABANDON: the chain was rejected); k2done /
+// k2need: K2's finished workgroups (the literals) in HBM.
+constexpr uint32_t K4F_PROG_FINAL = 0x7FFFFFFFu, K4F_PROG_ABANDON = 0xFFFFFFFFu;
+struct K4Fuse {
+  const volatile l_u32* prog;
+  const uint32_t* k2done;
+  uint32_t k2need;
+  uint32_t frame;
+};
+__device__ inline bool k4f_wait_k2(const K4Fuse& z) {
+  if (!z.k2need) return true;
+  // relaxed polls (an acquire per poll would invalidate the caches every
+  // time, under the chains running beside), one acquire fence at the end
+  for (uint32_t it = 0; it < (1u << 22); it++) {
+    if (__hip_atomic_load(z.k2done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= z.k2need) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(32);
+  }
+  return false;                               // (bounded: the frame goes to the redo pass)
+}
+// records [0, rec_end) complete (whole 16-record lines); false: abandon
+__device__ inline bool k4f_wait_recs(const K4Fuse& z, uint32_t rec_end) {
+  const uint32_t need = (rec_end + 15) >> 4;
+  for (uint32_t it = 0; it < (1u << 22); it++) {
+    const uint32_t v = *z.prog;
+    if (v == K4F_PROG_ABANDON) return false;
+    if (v >= need) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+template <bool FZ>
+__device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __restrict__ src, uint8_t* outbase,
                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
                                                    const BlockRec* __restrict__ blocks,
                                                    const CompBlock* __restrict__ comp,
@@ -2035,16 +2103,17 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                                                    const uint8_t* __restrict__ lits,
                                                    const uint64_t* __restrict__ seqs,
                                                    const uint16_t* __restrict__ fses, uint32_t f_begin,
-                                                   uint32_t f_end) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
-  __shared__ __attribute__((aligned(16))) uint8_t pat[64];
-  __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];   // LL | OF | ML symbols of the block
-  __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
-  const int lane = threadIdx.x;
+                                                   uint32_t f_end, uint32_t f_step, const uint8_t* __restrict__ redo,
+                                                   const K4Lds& M, const K4Fuse* fz, uint8_t* redo_out) {
+  l_u8* const win = M.win;
+  l_u8* const pat = M.pat;
+  l_u8* const stg = M.stg;
+  const int lane = threadIdx.x & 63;
 #if ZD_K4_CODELUT
   // LL | ML code -> baseline | extra-bit count << 24 (ll_code / ml_code,
   // sequences.rs tables), one LDS read per code instead of ~20 VALU ops
-  __shared__ uint32_t codelut[2][64];
+  l_u32 (*codelut)[64] = (l_u32 (*)[64])M.codelut;
+  l_u8 (*stab)[FSE_TAB] = (l_u8 (*)[FSE_TAB])M.stab;
   {
     uint32_t b, e;
     ll_code((uint32_t)lane, &b, &e);
@@ -2054,11 +2123,17 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     k4_sync();
   }
 #endif
+#if !ZD_K4_CODELUT
+  l_u8 (*stab)[FSE_TAB] = (l_u8 (*)[FSE_TAB])M.stab;
+#endif
   // persistent over frames when the grid is capped
-  for (uint32_t f = f_begin + blockIdx.x; f < f_end; f += gridDim.x) {
+  for (uint32_t f = f_begin; f < f_end; f += f_step) {
+  if (redo && !redo[f]) continue;                // the redo pass after zd_k_fused: its flagged frames only
   const FrameDesc F = frames[f];
-  if (F.lds) continue;                           // K4F executes this frame
+  if (F.lds) continue;                           // K4F / K4J execute this frame
   FrameState* S = &fstate[f];
+  bool abandoned = false;                        // fused mode: the frame goes to the redo pass
+  if constexpr (FZ) abandoned = !k4f_wait_k2(*fz);   // (K1's Huffman half and K2 have run: keys final)
   const uint64_t key0 = S->key;
   if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) continue;
 
@@ -2078,7 +2153,7 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     k4_sync();
   }
   uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
-  uint64_t err_key = KEY_NONE;
+  uint64_t err_key = abandoned ? 0 : KEY_NONE;
   // HBM holds [0, fl_safe) with every store completed (the bytes two batches
   // back); fl_last = the flush boundary after the previous batch
   int32_t fl_safe = X.fl;
@@ -2149,6 +2224,9 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
       return (lit_stage && 16 * (uint32_t)lane < K4_STG && cur + 16 * (uint32_t)lane < nl) ? ldg16_once(lsrc + cur + 16 * lane) : f4;
     };
     for (uint32_t s0 = 0; s0 < n && err_key == KEY_NONE;) {
+      if constexpr (FZ) {
+        if (!k4f_wait_recs(*fz, min(n_ld, s0 + 128))) { abandoned = true; err_key = 0; break; }
+      }
       const bool odd0 = !direct && (s0 & 1);        // a restart at an odd record
       const uint32_t vlim = odd0 ? s0 + 1 : n;       // (that record alone)
       uint64_t recA = odd0 ? (lane == 0 ? rec_get(SQ, s0, false) : 0) : rec_of(rec_at(s0 + lane));
@@ -2175,6 +2253,9 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
         // the next batch's windows and the records after it, first thing
         const uint64_t recBv = rec_of(recB);
         const WinU winB = win_of(recBv, s0 + 64 + lane < n);
+        if constexpr (FZ) {
+          if (!k4f_wait_recs(*fz, min(n_ld, s0 + 192))) { abandoned = true; err_key = 0; break; }
+        }
         const uint64_t recC = rec_at(s0 + 128 + lane);
         k4_flush(X, false);
         // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
@@ -2409,7 +2490,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
       err_key = make_key(PH_LIMIT, j, LS_CAPACITY, n, ZD_E_OUT_OF_DOMAIN);
   }
   if (err_key != KEY_NONE) {
-    if (lane == 0) key_min(fstate, f, err_key);
+    if (lane == 0) {
+      if (abandoned) redo_out[f] = 1;
+      else key_min(fstate, f, err_key);
+    }
+    k4_sync();
     continue;
   }
   k4_flush(X, true);
@@ -2427,6 +2512,139 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
     S->rep[2] = rep[2];
   }
   k4_sync();                               // the window is reused by the next frame
+  }
+}
+
+__global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __restrict__ src, uint8_t* outbase,
+                                                   const FrameDesc* __restrict__ frames, FrameState* fstate,
+                                                   const BlockRec* __restrict__ blocks,
+                                                   const CompBlock* __restrict__ comp,
+                                                   const CompState* __restrict__ cstate,
+                                                   const uint8_t* __restrict__ lits,
+                                                   const uint64_t* __restrict__ seqs,
+                                                   const uint16_t* __restrict__ fses, uint32_t f_begin,
+                                                   uint32_t f_end, const uint8_t* __restrict__ redo) {
+  __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
+  __shared__ __attribute__((aligned(16))) uint8_t pat[64];
+  __shared__ __attribute__((aligned(16))) uint8_t stab[3 * FSE_TAB];   // LL | OF | ML symbols of the block
+  __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
+  __shared__ uint32_t codelut[2 * 64];
+  const K4Lds M{(l_u8*)win, (l_u8*)pat, (l_u8*)stab, (l_u8*)stg, (l_u32*)codelut};
+  k4_body<false>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f_begin + blockIdx.x, f_end,
+                 gridDim.x, redo, M, nullptr, nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// zd_k_fused: K3 and K4 of FZ_FRAMES single-block frames in one workgroup, for
+// plans of few such frames (C3), where K3 is one round of chains and a K4
+// launch after it would leave every frame waiting for the longest chain.
+// Wave 0 runs K3Q for the frames' blocks (quads 0-3), publishing each chain's
+// completed 16-record lines to LDS (seq_chainq PUB); wave 1 + q runs K4 for
+// frame q (k4_body FZ), waiting for K2's literals (zd_k_huffman counts its
+// workgroups in k2done, released at agent scope) and for its records line by
+// line, so K4 runs behind the chain instead of after all chains.  Records and
+// literals never share a 128-byte line between blocks in such plans, and a
+// K4 wave reads a line only once it is complete, so the wave's caches hold no
+// stale record or literal.  A chain the fast path rejects (or a wait past its
+// bound) flags its frame in `redo`: the K4 wave abandons the frame without
+// writing its state, and the redo pass (K3Q + K4 over the flagged frames,
+// after this kernel) decodes it as the unfused pipeline would.
+// ---------------------------------------------------------------------------
+constexpr int FZ_FRAMES = 4;
+__global__ __launch_bounds__(64 * (1 + FZ_FRAMES)) void zd_k_fused(
+    const uint8_t* __restrict__ src, uint8_t* outbase, const FrameDesc* __restrict__ frames, FrameState* fstate,
+    const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp, CompState* cstate,
+    const uint8_t* __restrict__ lits, uint64_t* __restrict__ seqs, const uint16_t* __restrict__ fses,
+    uint32_t n_frames, const uint32_t* k2done, uint32_t k2need, uint8_t* redo) {
+  __shared__ __attribute__((aligned(16))) uint16_t tabs[FZ_FRAMES * K3_TAB];
+  __shared__ __attribute__((aligned(16))) uint8_t win[FZ_FRAMES][K4_C];
+  __shared__ __attribute__((aligned(16))) uint8_t pat[FZ_FRAMES][64];
+  __shared__ __attribute__((aligned(16))) uint8_t stab[FZ_FRAMES][3 * FSE_TAB];
+  __shared__ __attribute__((aligned(16))) uint8_t stg[FZ_FRAMES][K4_STG + 16];
+  __shared__ uint32_t codelut[FZ_FRAMES][2 * 64];
+  __shared__ uint32_t prog[FZ_FRAMES];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x < FZ_FRAMES) prog[threadIdx.x] = 0;
+  __syncthreads();
+  if (wave > 0) {
+    const int q = wave - 1;
+    const uint32_t f = blockIdx.x * FZ_FRAMES + q;
+    if (f >= n_frames) return;
+    const K4Lds M{(l_u8*)win[q], (l_u8*)pat[q], (l_u8*)stab[q], (l_u8*)stg[q], (l_u32*)codelut[q]};
+    const K4Fuse z{(const volatile l_u32*)&prog[q], k2done, k2need, f};
+    k4_body<true>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f, f + 1, 1, nullptr, M, &z,
+                  redo);
+    return;
+  }
+  // wave 0: the chains (quad q: frame blockIdx.x * FZ_FRAMES + q)
+  const int role = lane & 3, q = lane >> 2;
+  const uint32_t f = blockIdx.x * FZ_FRAMES + q;
+  const bool mine = q < FZ_FRAMES && f < n_frames;
+  bool act = mine;
+  uint32_t ci = 0;
+  CompBlock C;
+  if (act) {
+    const FrameDesc F = frames[f];
+    const int32_t c = F.nblocks ? blocks[F.first_block].comp : -1;
+    act = c >= 0;
+    ci = act ? (uint32_t)c : 0;
+  }
+  if (act) C = comp[ci];
+  if (act) {
+    const uint64_t key0 = fstate[f].key;
+    // the blocks zd_k_sequences_q would run (list_seq, and its PH_PARSE skip)
+    act = C.nseq > 0 && C.tab_src[0] >= 0 && C.tab_src[1] >= 0 && C.tab_src[2] >= 0 &&
+          !(key0 != KEY_NONE && key_phase(key0) == PH_PARSE);
+  }
+  int al[3] = {0, 0, 0};
+  const uint16_t* g[3] = {nullptr, nullptr, nullptr};
+  if (act) {
+    for (int k = 0; k < 3; k++) {
+      const uint32_t sidx = (uint32_t)C.tab_src[k];
+      al[k] = cstate[sidx].al[k];
+      g[k] = fses + (uint64_t)comp[sidx].fse_slot * FSE_SLOT + k * FSE_TAB;
+    }
+  }
+  const bool use_lds = __ballot(act && al[1] > 8) == 0;
+  lds_u16* mine_t = (lds_u16*)tabs + (q < FZ_FRAMES ? q : 0) * K3_TAB;
+  if (use_lds && act && role < 3) {
+    const int dst[3] = {0, K3_TL + K3_TM, K3_TL};     // LL | ML | OF in LDS
+    const int k = role;
+    const int cnt = 1 << al[k];
+    if (cnt >= 8) {
+      typedef __attribute__((address_space(1))) const u32x4 g_u4;
+      typedef __attribute__((address_space(3))) u32x4 l_u4;
+      g_u4* s4 = (g_u4*)g[k];
+      l_u4* d4 = (l_u4*)(mine_t + dst[k]);
+      for (int e = 0; e < cnt / 8; e++) {
+        u32x4 v = s4[e];
+        v.x = K3_ENTRY(v.x & 0xFFFF, k, al[k]) | (K3_ENTRY(v.x >> 16, k, al[k]) << 16);
+        v.y = K3_ENTRY(v.y & 0xFFFF, k, al[k]) | (K3_ENTRY(v.y >> 16, k, al[k]) << 16);
+        v.z = K3_ENTRY(v.z & 0xFFFF, k, al[k]) | (K3_ENTRY(v.z >> 16, k, al[k]) << 16);
+        v.w = K3_ENTRY(v.w & 0xFFFF, k, al[k]) | (K3_ENTRY(v.w >> 16, k, al[k]) << 16);
+        d4[e] = v;
+      }
+    } else {
+      for (int e = 0; e < cnt; e++) mine_t[dst[k] + e] = (uint16_t)K3_ENTRY(((g_u16*)g[k])[e], k, al[k]);
+    }
+  }
+  k4_sync();
+  int rej = 0;
+  if (act) {
+    if (use_lds) {
+      const CompState cs = cstate[ci];
+      const lds_u16* tab = role == 0 ? mine_t + K3_TL + K3_TM : role == 1 ? mine_t + K3_TL : mine_t;
+      rej = seq_chainq<ZD_K3_LA, ZD_K3_WN, true>(src + C.src + cs.bs_off, cs.bs_size, (uintptr_t)src, tab, role,
+                                                 al[0], al[1], al[2], C.nseq, seqs + C.seq_out,
+                                                 (volatile __attribute__((address_space(3))) uint32_t*)&prog[q]);
+    } else {
+      rej = 1;                                   // OF tables deeper than LDS holds: the redo pass
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (mine && role == 0) {
+    if (rej) redo[f] = 1;
+    *(volatile uint32_t*)&prog[q] = rej ? K4F_PROG_ABANDON : K4F_PROG_FINAL;
   }
 }
 
@@ -3573,26 +3791,27 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
   if (a.n_huf)
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s2, a.src, comp,
-                       cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits);
+                       cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits,
+                       (a.fused && fork) ? (uint32_t*)(ws + W.k2done) : (uint32_t*)nullptr);
   if (fork)
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
-  auto k3 = [&](const uint32_t* list, uint32_t n, hipStream_t st) {
+  auto k3 = [&](const uint32_t* list, uint32_t n, hipStream_t st, const uint8_t* redo) {
     if (n) {
       if (a.k3_quad)
         hipLaunchKernelGGL(zd_k_sequences_q, dim3((n + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, st, a.src, comp,
-                           cstate, fstate, list, n, (const uint16_t*)fses, seqs);
+                           cstate, fstate, list, n, (const uint16_t*)fses, seqs, redo);
       else
         hipLaunchKernelGGL(zd_k_sequences, dim3((n + K3_LANES - 1) / K3_LANES), dim3(K3_LANES), 0, st, a.src, comp,
                            cstate, fstate, list, n, (const uint16_t*)fses, seqs);
     }
   };
-  auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st) {
+  auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st, const uint8_t* redo) {
     const uint32_t n = f1 - f0;
     if (n && a.n_frames > a.n_k4f)   // frames on the streaming K4 (K4F's exit at once)
       hipLaunchKernelGGL(zd_k_execute, dim3(n),
                          dim3(64), 0, st, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
-                         (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1);
+                         (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1, redo);
   };
   auto k4f = [&](const uint32_t* list, uint32_t n, hipStream_t st) {
     if (n)
@@ -3600,12 +3819,27 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                          (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                          (const uint16_t*)fses, list);
   };
-  k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s);
-  if (fork)
-    if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
-  if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
-  k4(0, a.n_frames, s);
-  k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s);
+  if (a.fused && !a.events) {
+    // K3 + K4 per group of four frames; K2 (forked) signals its workgroups;
+    // then the redo pass for the frames the fused kernel flagged (normally none:
+    // two launches whose workgroups exit at once)
+    uint8_t* redo = ws + W.redo;
+    const uint32_t k2need = fork ? (a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS : 0;
+    hipLaunchKernelGGL(zd_k_fused, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * (1 + FZ_FRAMES)), 0, s,
+                       a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
+                       (const uint16_t*)fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
+    if (fork)
+      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
+    k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, redo);
+    k4(0, a.n_frames, s, redo);
+  } else {
+    k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, nullptr);
+    if (fork)
+      if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
+    if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
+    k4(0, a.n_frames, s, nullptr);
+    k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s);
+  }
   if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;
   if (a.n_jframes) {
     auto* jframes = (const JFrame*)(ws + W.jframes);

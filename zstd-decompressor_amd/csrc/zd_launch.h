@@ -23,6 +23,7 @@ struct LaunchArgs {
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
   bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block
   uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
+  bool fused = false;                      // K3 + K4 as zd_k_fused, then the redo pass
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.

@@ -176,3 +176,4 @@ F_SKIPPABLE = 1
 F_BLOCK_PARALLEL = 2   # every frame with a compressed block -> K4J (block-parallel execute)
 F_FRAME_SERIAL = 4     # no frame -> K4J
 F_SEQ_ONE_LANE = 8     # K3 one lane per block instead of four (K3Q)
+F_NO_FUSE = 32         # K3 then K4 as two launches in few-frame plans (no zd_k_fused)
