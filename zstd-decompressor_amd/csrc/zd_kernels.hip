@@ -2082,6 +2082,9 @@ __device__ inline bool k4f_wait_k2(const K4Fuse& z) {
   }
   return false;                               // (bounded: the frame goes to the redo pass)
 }
+#ifndef ZD_FZ_SLEEP
+#define ZD_FZ_SLEEP 2
+#endif
 // records [0, rec_end) complete (whole 16-record lines); false: abandon
 __device__ inline bool k4f_wait_recs(const K4Fuse& z, uint32_t rec_end) {
   const uint32_t need = (rec_end + 15) >> 4;
@@ -2089,7 +2092,7 @@ __device__ inline bool k4f_wait_recs(const K4Fuse& z, uint32_t rec_end) {
     const uint32_t v = *z.prog;
     if (v == K4F_PROG_ABANDON) return false;
     if (v >= need) return true;
-    __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_s_sleep(ZD_FZ_SLEEP);
   }
   return false;
 }
