@@ -492,7 +492,8 @@ constexpr size_t FUSE_MIN_FRAMES = 256;
 bool fuse_plan(const zd_plan* P, uint64_t out_len0) {
   static const char* env = getenv("ZD_FUSE");
   if (env && atoi(env) == 0) return false;
-  if ((P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) || out_len0) return false;
+  if ((P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) || out_len0 || P->has_prebuilt)
+    return false;
   const size_t cus = k3_slots() / 64;
   if (P->nframes < (env ? 1 : FUSE_MIN_FRAMES) || P->nframes > 4 * cus) return false;
   for (const HostPart& hp : P->parts)

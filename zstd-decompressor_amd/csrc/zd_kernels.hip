@@ -207,6 +207,15 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
 // a 16-bit entry (zd_common.h fse_entry); nbits/baseline follow from it and
 // equal the reference's parts/base_width construction (fse.rs:169-189).
 // `-1` symbols count as 1.  sym/next are LDS scratch (T and 256 entries).
+#ifdef ZD_FZ_TRACE
+// zd_k_fused timeline (scripts/fztrace.py): per frame s_memrealtime at the
+// kernel's start, tables ready, chain end, K4's waits over, K4 end; K2's end
+__device__ uint64_t fz_tr[1024][8];
+__device__ uint64_t fz_k2end;
+#define FZT(f, i) do { if ((f) < 1024) fz_tr[f][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define FZT(f, i) do { } while (0)
+#endif
 #ifdef ZD_K1_PROF
 __device__ uint64_t k1_prof[8];
 #define K1T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -1189,6 +1198,9 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
   if (k2done) {
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(k2done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef ZD_FZ_TRACE
+    if (threadIdx.x == 0) atomicMax((unsigned long long*)&fz_k2end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
   }
 }
 
@@ -1582,6 +1594,9 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
+#ifndef ZD_FZ_PUB
+#define ZD_FZ_PUB 16                 // records between publications (a multiple of 16)
+#endif
 template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
@@ -1661,7 +1676,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
       outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
       if constexpr (PUB) {
-        if (((slot + 2) & 15) == 0 && slot + 2 >= 32) {
+        if (((slot + 2) & (ZD_FZ_PUB - 1)) == 0 && slot + 2 >= 32) {
           asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
           if (role == 0) *prog = (slot + 2 - 16) >> 4;
         }
@@ -2065,26 +2080,37 @@ struct K4Lds {
 constexpr uint32_t K4F_PROG_FINAL = 0x7FFFFFFFu, K4F_PROG_ABANDON = 0xFFFFFFFFu;
 struct K4Fuse {
   const volatile l_u32* prog;
+  const volatile l_u32* trdy;                 // nonzero: the block's sequence tables are in HBM
   const uint32_t* k2done;
   uint32_t k2need;
   uint32_t frame;
 };
-__device__ inline bool k4f_wait_k2(const K4Fuse& z) {
-  if (!z.k2need) return true;
-  // relaxed polls (an acquire per poll would invalidate the caches every
-  // time, under the chains running beside), one acquire fence at the end
-  for (uint32_t it = 0; it < (1u << 22); it++) {
-    if (__hip_atomic_load(z.k2done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= z.k2need) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      return true;
-    }
-    __builtin_amdgcn_s_sleep(32);
-  }
-  return false;                               // (bounded: the frame goes to the redo pass)
-}
 #ifndef ZD_FZ_SLEEP
 #define ZD_FZ_SLEEP 2
 #endif
+// The frame's sequence tables (wave 0 of zd_k_fused builds them, with their
+// CompState bytes and any parse error key), then K2's literals.  Relaxed
+// polls (an acquire per poll would invalidate the caches every time, under
+// the chains running beside), one acquire fence at the end: it also drops
+// the CU's copy of the frame's key line, which wave 0 read before its
+// key_min (an L2 atomic).  false: a wait ran past its bound, the frame goes
+// to the redo pass.
+__device__ inline bool k4f_wait_k2(const K4Fuse& z) {
+  bool ok = false;
+  for (uint32_t it = 0; it < (1u << 22) && !ok; it++) {
+    ok = *z.trdy != 0;
+    if (!ok) __builtin_amdgcn_s_sleep(ZD_FZ_SLEEP);
+  }
+  if (ok && z.k2need) {
+    ok = false;
+    for (uint32_t it = 0; it < (1u << 22) && !ok; it++) {
+      ok = __hip_atomic_load(z.k2done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= z.k2need;
+      if (!ok) __builtin_amdgcn_s_sleep(32);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return ok;
+}
 // records [0, rec_end) complete (whole 16-record lines); false: abandon
 __device__ inline bool k4f_wait_recs(const K4Fuse& z, uint32_t rec_end) {
   const uint32_t need = (rec_end + 15) >> 4;
@@ -2136,7 +2162,8 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
   if (F.lds) continue;                           // K4F / K4J execute this frame
   FrameState* S = &fstate[f];
   bool abandoned = false;                        // fused mode: the frame goes to the redo pass
-  if constexpr (FZ) abandoned = !k4f_wait_k2(*fz);   // (K1's Huffman half and K2 have run: keys final)
+  if constexpr (FZ) abandoned = !k4f_wait_k2(*fz);   // (K1 and K2 have run: keys final)
+  if (FZ && lane == 0) FZT(f, 3);
   const uint64_t key0 = S->key;
   if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) continue;
 
@@ -2501,6 +2528,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
     continue;
   }
   k4_flush(X, true);
+  if (FZ && lane == 0) FZT(f, 4);
 #ifdef ZD_K4_PROF
   if (lane == 0 && f < 3)
     printf("K4 frame %u batches %llu rounds %llu: rec/val %llu scan/rep %llu chk/lit %llu far %llu rounds %llu flush %llu top %llu\n", f,
@@ -2538,12 +2566,14 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
 }
 
 // ---------------------------------------------------------------------------
-// zd_k_fused: K3 and K4 of FZ_FRAMES single-block frames in one workgroup, for
-// plans of few such frames (C3), where K3 is one round of chains and a K4
-// launch after it would leave every frame waiting for the longest chain.
-// Wave 0 runs K3Q for the frames' blocks (quads 0-3), publishing each chain's
-// completed 16-record lines to LDS (seq_chainq PUB); wave 1 + q runs K4 for
-// frame q (k4_body FZ), waiting for K2's literals (zd_k_huffman counts its
+// zd_k_fused: K1's sequence half, K3 and K4 of FZ_FRAMES single-block frames
+// in one workgroup, for plans of few such frames (C3), where K3 is one round
+// of chains and a K4 launch after it would leave every frame waiting for the
+// longest chain.  Wave 0 builds the blocks' FSE tables (quad q, lane k < 3:
+// table k of frame q, straight into LDS; zd_k_tables PART 2 is not launched)
+// and runs K3Q on them, publishing each chain's completed 16-record lines to
+// LDS (seq_chainq PUB); wave 1 + q runs K4 for frame q (k4_body FZ), waiting
+// for the tables (trdy), for K2's literals (zd_k_huffman counts its
 // workgroups in k2done, released at agent scope) and for its records line by
 // line, so K4 runs behind the chain instead of after all chains.  Records and
 // literals never share a 128-byte line between blocks in such plans, and a
@@ -2551,13 +2581,224 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
 // stale record or literal.  A chain the fast path rejects (or a wait past its
 // bound) flags its frame in `redo`: the K4 wave abandons the frame without
 // writing its state, and the redo pass (K3Q + K4 over the flagged frames,
-// after this kernel) decodes it as the unfused pipeline would.
+// after this kernel, on the tables this kernel left in HBM) decodes it as the
+// unfused pipeline would.
 // ---------------------------------------------------------------------------
-constexpr int FZ_FRAMES = 4;
-__global__ __launch_bounds__(64 * (1 + FZ_FRAMES)) void zd_k_fused(
+// The K4 waves' build of their blocks' sequence tables (K1's sequence half,
+// zd_k_tables PART 2, for the fused plans): the wave is idle until K2's
+// literals anyway, and 64 lanes build a table far sooner than one lane's
+// serial walk, which put K1's sequence half (0.25 ms) before every chain.
+struct FzK1 {
+  int16_t dist[3][256];
+  uint16_t tab[3][FSE_TAB];          // compact entries (the slot format)
+  uint16_t cum[260];                 // placements before each symbol
+  uint16_t cnt[256];                 // nextState counters
+  uint8_t sym[FSE_TAB];
+};
+struct FzInfo {                      // a block's table results, for wave 0
+  uint32_t al;                       // LL | OF << 8 | ML << 16
+  uint32_t err;                      // first failure: sub << 8 | -code (0: none)
+  uint32_t bo, bsz;                  // sequence bitstream
+};
+constexpr uint32_t FZ_DESC = 2048;   // description bytes staged in LDS (three tables need <= ~1.3 KB)
+
+__device__ inline uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// FseTable::from_distribution (fse.rs:110-202) by a whole wave, with
+// build_fse's results and errors.  The spread visits positions j * step &
+// mask (a permutation of the states: step is odd), skipping the -1 symbols'
+// top positions, so placement r in symbol order lands on the r-th such
+// position below zero_pos: each lane takes positions j and finds its
+// symbol from the placement's rank (a search over the cumulative counts).
+// nextState of state i is count(s) plus the earlier states of s: per 64
+// states, one round per distinct symbol.
+__device__ int fz_build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* tab, FzK1& W, int lane) {
+  if (al > FSE_MAX_AL) return ZD_E_LARGE_ACCURACY_LOG;
+  const uint32_t T = 1u << al, mask = T - 1, step = (T >> 1) + (T >> 3) + 3;
+  uint32_t nneg = 0, placed = 0;
+  for (uint32_t b = 0; b < nsym; b += 64) {
+    const uint32_t s = b + lane;
+    const int c = s < nsym ? dist[s] : 0;
+    const uint64_t neg = __ballot(c == -1);
+    if (c == -1) {                             // build_fse's first loop: sym[--zero_pos] = s
+      const uint32_t m = nneg + lanes_below(neg);
+      if (m < T) W.sym[T - 1 - m] = (uint8_t)s;
+    }
+    const uint32_t pc = c > 0 ? (uint32_t)c : 0u;
+    const uint32_t inc = wave_scan_incl(pc);
+    if (s < nsym) W.cum[s] = (uint16_t)(placed + inc - pc);
+    placed += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    nneg += (uint32_t)__popcll(neg);
+  }
+  if (nneg > T) return ZD_E_REF_PANIC;
+  const uint32_t zero_pos = T - nneg;
+  if (placed > 0 && zero_pos == 0) return ZD_E_REF_PANIC;   // the reference loops forever
+  if (placed != zero_pos) return ZD_E_CORRUPTED_TABLE;
+  k4_sync();
+  uint32_t rbase = 0;
+  for (uint32_t j0 = 0; j0 < T; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const uint32_t x = (j * step) & mask;
+    const bool v = j < T && x < zero_pos;
+    const uint64_t bm = __ballot(v);
+    if (v) {
+      const uint32_t r = rbase + lanes_below(bm);
+      uint32_t lo = 0, hi = nsym;                // the last symbol with cum <= r
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (W.cum[mid] <= r) lo = mid; else hi = mid;
+      }
+      W.sym[x] = (uint8_t)lo;
+    }
+    rbase += (uint32_t)__popcll(bm);
+  }
+  for (uint32_t s = lane; s < nsym; s += 64) {
+    const int c = dist[s];
+    W.cnt[s] = (uint16_t)(c > 0 ? c : (c == -1 ? 1 : 0));
+  }
+  k4_sync();
+  for (uint32_t i0 = 0; i0 < T; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t s = i < T ? W.sym[i] : 0u;
+    uint64_t rem = __ballot(i < T);
+    uint32_t ns = 0;
+    while (rem) {
+      const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)__builtin_ctzll(rem));
+      const uint64_t m = __ballot(s == sl) & rem;
+      const uint32_t base = W.cnt[sl];
+      if ((m >> lane) & 1) ns = base + lanes_below(m);
+      k4_sync();
+      if (lane == 0) W.cnt[sl] = (uint16_t)(base + (uint32_t)__popcll(m));
+      k4_sync();
+      rem &= ~m;
+    }
+    if (i < T) tab[i] = fse_entry(s, ns);
+  }
+  k4_sync();
+  return 0;
+}
+
+// A K4 wave's block: k1_sequences_lane's walk (sequences.rs:91-187) with the
+// descriptions parsed by lane 0 from an LDS copy and each table built by the
+// wave; then what zd_k_tables leaves (the tables the serial walk completes
+// in the block's slot, their accuracy logs, the bitstream, a parse error's
+// key), the K3 tables for wave 0 (tabs, when they fit) and the block's
+// FzInfo.  Every lane returns.
+__device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* __restrict__ src, const CompBlock& C, uint32_t ci, CompState* cstate,
+                          FrameState* fstate, uint16_t* fses, FzK1& W, l_u8* desc, lds_u16* k3tab, FzInfo& I,
+                          int lane) {
+  // the description bytes (<= FZ_DESC: NCount descriptions of <= 255
+  // symbols of <= 10 bits each take <= 410 bytes, the RLE bytes one)
+  const uint32_t base = C.seq_tables;
+  const uint32_t avail = C.size > base ? C.size - base : 0u;
+  const uint32_t ncopy = avail < FZ_DESC ? avail : FZ_DESC;
+  for (uint32_t x = lane; x < ncopy; x += 64) desc[x] = src[C.src + base + x];
+  k4_sync();
+  // lane 0: the descriptions in order; results by readlane
+  int pst = 0, psub = 3;
+  uint32_t alp = 0, nsp = 0, rle = 0, pos = base;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (pst) break;
+      const int mode = C.modes[k];
+      int st = 0, al = 0;
+      uint32_t nsym = 0;
+      if (mode == M_RLE) {
+        if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
+        else { rle |= (uint32_t)desc[pos - base] << (8 * k); pos++; }
+      } else if (mode == M_FSE) {
+        if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
+        else {
+          FwBits fw{(const uint8_t*)(desc + (pos - base)), C.size - pos, 0};
+          uint8_t a = 0;
+          st = parse_ncount(fw, &a, W.dist[k], &nsym, 256);
+          al = a;
+          pos += fw.bytes_read();
+        }
+      } else if (mode == M_PREDEFINED) {
+        al = k == 1 ? 5 : 6;
+        nsym = k == 0 ? 36 : (k == 1 ? 29 : 53);
+      }
+      if (st) { pst = st; psub = k; }
+      alp |= (uint32_t)al << (8 * k);
+      nsp |= nsym << (9 * k);
+    }
+  }
+  pst = __builtin_amdgcn_readfirstlane(pst);
+  psub = __builtin_amdgcn_readfirstlane(psub);
+  alp = (uint32_t)__builtin_amdgcn_readfirstlane((int)alp);
+  nsp = (uint32_t)__builtin_amdgcn_readfirstlane((int)nsp);
+  rle = (uint32_t)__builtin_amdgcn_readfirstlane((int)rle);
+  pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
+  k4_sync();
+  // the tables before the first parse failure, in order; a build failure
+  // stops the walk there
+  int fst = pst, fsub = pst ? psub : 4;
+  // (modes packed: an index into C would put it in scratch)
+  const uint32_t modes = (uint32_t)C.modes[0] | (uint32_t)C.modes[1] << 8 | (uint32_t)C.modes[2] << 16;
+  for (int k = 0; k < 3 && k < psub; k++) {
+    const int mode = (int)((modes >> (8 * k)) & 255);
+    const int al = (int)((alp >> (8 * k)) & 255);
+    const uint32_t nsym = (nsp >> (9 * k)) & 511;
+    int st = 0;
+    if (mode == M_RLE) {
+      if (lane == 0) W.tab[k][0] = fse_entry((rle >> (8 * k)) & 255, 1);   // AL 0: nb 0, baseline 0
+    } else if (mode == M_FSE || mode == M_PREDEFINED) {
+      if (mode == M_PREDEFINED) {
+        const int16_t* d = k == 0 ? c_ll_default : (k == 1 ? c_of_default : c_ml_default);
+        for (uint32_t x = lane; x < nsym; x += 64) W.dist[k][x] = d[x];
+        k4_sync();
+      }
+      st = fz_build_fse(al, W.dist[k], nsym, W.tab[k], W, lane);
+    }
+    if (st) { fst = st; fsub = k; break; }
+  }
+  k4_sync();
+  if (!fst && pos >= C.size) { fst = ZD_E_EMPTY_SLICE; fsub = 3; }   // seq.bitstream of the empty rest
+  const uint32_t bo = fsub >= 3 ? pos : 0u;
+  const uint32_t bsz = fsub >= 3 && pos < C.size ? C.size - pos : 0u;
+  const int dst[3] = {0, K3_TL + K3_TM, K3_TL};      // wave 0's LL | ML | OF
+  const int cap[3] = {K3_TL, K3_TO, K3_TM};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int mode = (int)((modes >> (8 * k)) & 255);
+    if (fsub <= k || mode == M_REPEAT) continue;
+    const int al = (int)((alp >> (8 * k)) & 255);
+    const int cnt = mode == M_RLE ? 1 : 1 << al;
+    uint16_t* g = fses + (uint64_t)C.fse_slot * FSE_SLOT + k * FSE_TAB;
+    for (int e = lane; e < cnt; e += 64) {
+      const uint32_t v = W.tab[k][e];
+      g[e] = (uint16_t)v;
+      if (cnt <= cap[k]) k3tab[dst[k] + e] = (uint16_t)K3_ENTRY(v, k, al);
+    }
+    if (lane == 0) cstate[ci].al[k] = (uint8_t)al;
+  }
+  if (lane == 0) {
+    cstate[ci].bs_off = bo;
+    cstate[ci].bs_size = bsz;
+    if (fst) key_min(fstate, C.frame, make_key(PH_PARSE, C.block_in_frame, PS_SEQ_TABLES, (uint32_t)fsub, fst));
+    I.al = alp;
+    I.err = fst ? ((uint32_t)fsub << 8) | (uint32_t)((-fst) & 0xFF) : 0u;
+    I.bo = bo;
+    I.bsz = bsz;
+  }
+}
+
+#ifndef ZD_FZ_SOLO
+#define ZD_FZ_SOLO 0                 // 1: eight waves, K4 frames on waves 1-3 and 5-7 (wave 4 idle)
+#endif
+#ifndef ZD_FZ_PRIO
+#define ZD_FZ_PRIO 0                 // the chain wave's s_setprio
+#endif
+constexpr int FZ_FRAMES = ZD_FZ_SOLO ? 6 : 4;
+constexpr int FZ_WAVES = ZD_FZ_SOLO ? 8 : 1 + FZ_FRAMES;
+__global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
     const uint8_t* __restrict__ src, uint8_t* outbase, const FrameDesc* __restrict__ frames, FrameState* fstate,
     const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp, CompState* cstate,
-    const uint8_t* __restrict__ lits, uint64_t* __restrict__ seqs, const uint16_t* __restrict__ fses,
+    const uint8_t* __restrict__ lits, uint64_t* __restrict__ seqs, uint16_t* __restrict__ fses,
     uint32_t n_frames, const uint32_t* k2done, uint32_t k2need, uint8_t* redo) {
   __shared__ __attribute__((aligned(16))) uint16_t tabs[FZ_FRAMES * K3_TAB];
   __shared__ __attribute__((aligned(16))) uint8_t win[FZ_FRAMES][K4_C];
@@ -2565,79 +2806,88 @@ __global__ __launch_bounds__(64 * (1 + FZ_FRAMES)) void zd_k_fused(
   __shared__ __attribute__((aligned(16))) uint8_t stab[FZ_FRAMES][3 * FSE_TAB];
   __shared__ __attribute__((aligned(16))) uint8_t stg[FZ_FRAMES][K4_STG + 16];
   __shared__ uint32_t codelut[FZ_FRAMES][2 * 64];
-  __shared__ uint32_t prog[FZ_FRAMES];
+  __shared__ uint32_t prog[FZ_FRAMES], trdy[FZ_FRAMES];
+  __shared__ __attribute__((aligned(16))) FzK1 k1w[FZ_FRAMES];
+  __shared__ FzInfo info[FZ_FRAMES];
+  static_assert(FZ_DESC <= K4_C, "the description copy lives in the K4 window");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (threadIdx.x < FZ_FRAMES) prog[threadIdx.x] = 0;
+  if (threadIdx.x < FZ_FRAMES) prog[threadIdx.x] = trdy[threadIdx.x] = 0;
   __syncthreads();
   if (wave > 0) {
-    const int q = wave - 1;
+    if (ZD_FZ_SOLO && (wave & 3) == 0) return;
+    const int q = ZD_FZ_SOLO ? wave - 1 - (wave >> 2) : wave - 1;
     const uint32_t f = blockIdx.x * FZ_FRAMES + q;
     if (f >= n_frames) return;
+    {
+      // the block's sequence tables (the window is free until the waits)
+      const FrameDesc F = frames[f];
+      const int32_t c = F.nblocks ? blocks[F.first_block].comp : -1;
+      bool build = false;
+      CompBlock C;
+      if (c >= 0) {
+        C = comp[c];
+        build = C.nseq > 0 && C.host_stage > PS_SEQ_TABLES && !C.prebuilt;
+      }
+      if (build) {
+        fz_tables(src, C, (uint32_t)c, cstate, fstate, fses, k1w[q], (l_u8*)win[q], (lds_u16*)tabs + q * K3_TAB,
+                  info[q], lane);
+      } else if (lane == 0) {
+        info[q] = FzInfo{0u, 0u, 0u, 0u};
+      }
+      // tables, CompState bytes and key in place before trdy (wave 0 and
+      // this wave's k4f_wait_k2 acquire after it)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) *(volatile uint32_t*)&trdy[q] = 1;
+      if (lane == 0) FZT(f, 1);
+      k4_sync();
+    }
     const K4Lds M{(l_u8*)win[q], (l_u8*)pat[q], (l_u8*)stab[q], (l_u8*)stg[q], (l_u32*)codelut[q]};
-    const K4Fuse z{(const volatile l_u32*)&prog[q], k2done, k2need, f};
+    const K4Fuse z{(const volatile l_u32*)&prog[q], (const volatile l_u32*)&trdy[q], k2done, k2need, f};
     k4_body<true>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f, f + 1, 1, nullptr, M, &z,
                   redo);
     return;
   }
   // wave 0: the chains (quad q: frame blockIdx.x * FZ_FRAMES + q)
+  if (ZD_FZ_PRIO) __builtin_amdgcn_s_setprio(ZD_FZ_PRIO);
   const int role = lane & 3, q = lane >> 2;
   const uint32_t f = blockIdx.x * FZ_FRAMES + q;
   const bool mine = q < FZ_FRAMES && f < n_frames;
-  bool act = mine;
-  uint32_t ci = 0;
-  CompBlock C;
-  if (act) {
+  const int q4 = q < FZ_FRAMES ? q : 0;
+  if (mine && role == 0) FZT(f, 0);
+  int32_t c = -1;
+  if (mine) {
     const FrameDesc F = frames[f];
-    const int32_t c = F.nblocks ? blocks[F.first_block].comp : -1;
-    act = c >= 0;
-    ci = act ? (uint32_t)c : 0;
+    c = F.nblocks ? blocks[F.first_block].comp : -1;
   }
-  if (act) C = comp[ci];
-  if (act) {
-    const uint64_t key0 = fstate[f].key;
-    // the blocks zd_k_sequences_q would run (list_seq, and its PH_PARSE skip)
-    act = C.nseq > 0 && C.tab_src[0] >= 0 && C.tab_src[1] >= 0 && C.tab_src[2] >= 0 &&
-          !(key0 != KEY_NONE && key_phase(key0) == PH_PARSE);
+  const uint32_t ci = c >= 0 ? (uint32_t)c : 0;
+  CompBlock C;
+  if (c >= 0) C = comp[ci];
+  const uint64_t key0 = mine ? fstate[f].key : KEY_NONE;
+  // the tables from the K4 waves
+  bool ready = false;
+  for (uint32_t it = 0; it < (1u << 22) && !ready; it++) {
+    ready = __ballot(mine && *(volatile uint32_t*)&trdy[q4] == 0) == 0;
+    if (!ready) __builtin_amdgcn_s_sleep(ZD_FZ_SLEEP);
   }
-  int al[3] = {0, 0, 0};
-  const uint16_t* g[3] = {nullptr, nullptr, nullptr};
-  if (act) {
-    for (int k = 0; k < 3; k++) {
-      const uint32_t sidx = (uint32_t)C.tab_src[k];
-      al[k] = cstate[sidx].al[k];
-      g[k] = fses + (uint64_t)comp[sidx].fse_slot * FSE_SLOT + k * FSE_TAB;
-    }
-  }
+  asm volatile("" ::: "memory");
+  FzInfo I = FzInfo{0u, 0u, 0u, 0u};
+  if (mine) I = info[q4];
+  const int al[3] = {(int)(I.al & 255), (int)((I.al >> 8) & 255), (int)((I.al >> 16) & 255)};
+  const bool build = c >= 0 && C.nseq > 0 && C.host_stage > PS_SEQ_TABLES && !C.prebuilt;
+  // the blocks zd_k_sequences_q would run (list_seq, and its PH_PARSE skip),
+  // on this block's own tables (a table from another block: the redo pass)
+  bool act = ready && build && I.err == 0 && C.tab_src[0] >= 0 && C.tab_src[1] >= 0 && C.tab_src[2] >= 0 &&
+             !(key0 != KEY_NONE && key_phase(key0) == PH_PARSE);
+  int rej = mine && !ready ? 1 : 0;
+  if (act && (C.tab_src[0] != c || C.tab_src[1] != c || C.tab_src[2] != c)) { act = false; rej = 1; }
   const bool use_lds = __ballot(act && al[1] > 8) == 0;
-  lds_u16* mine_t = (lds_u16*)tabs + (q < FZ_FRAMES ? q : 0) * K3_TAB;
-  if (use_lds && act && role < 3) {
-    const int dst[3] = {0, K3_TL + K3_TM, K3_TL};     // LL | ML | OF in LDS
-    const int k = role;
-    const int cnt = 1 << al[k];
-    if (cnt >= 8) {
-      typedef __attribute__((address_space(1))) const u32x4 g_u4;
-      typedef __attribute__((address_space(3))) u32x4 l_u4;
-      g_u4* s4 = (g_u4*)g[k];
-      l_u4* d4 = (l_u4*)(mine_t + dst[k]);
-      for (int e = 0; e < cnt / 8; e++) {
-        u32x4 v = s4[e];
-        v.x = K3_ENTRY(v.x & 0xFFFF, k, al[k]) | (K3_ENTRY(v.x >> 16, k, al[k]) << 16);
-        v.y = K3_ENTRY(v.y & 0xFFFF, k, al[k]) | (K3_ENTRY(v.y >> 16, k, al[k]) << 16);
-        v.z = K3_ENTRY(v.z & 0xFFFF, k, al[k]) | (K3_ENTRY(v.z >> 16, k, al[k]) << 16);
-        v.w = K3_ENTRY(v.w & 0xFFFF, k, al[k]) | (K3_ENTRY(v.w >> 16, k, al[k]) << 16);
-        d4[e] = v;
-      }
-    } else {
-      for (int e = 0; e < cnt; e++) mine_t[dst[k] + e] = (uint16_t)K3_ENTRY(((g_u16*)g[k])[e], k, al[k]);
-    }
-  }
-  k4_sync();
-  int rej = 0;
+  lds_u16* mine_t = (lds_u16*)tabs + q4 * K3_TAB;
+  if (mine && role == 0) FZT(f, 5);
   if (act) {
     if (use_lds) {
-      const CompState cs = cstate[ci];
       const lds_u16* tab = role == 0 ? mine_t + K3_TL + K3_TM : role == 1 ? mine_t + K3_TL : mine_t;
-      rej = seq_chainq<ZD_K3_LA, ZD_K3_WN, true>(src + C.src + cs.bs_off, cs.bs_size, (uintptr_t)src, tab, role,
+      rej = seq_chainq<ZD_K3_LA, ZD_K3_WN, true>(src + C.src + I.bo, I.bsz, (uintptr_t)src, tab, role,
                                                  al[0], al[1], al[2], C.nseq, seqs + C.seq_out,
                                                  (volatile __attribute__((address_space(3))) uint32_t*)&prog[q]);
     } else {
@@ -2645,6 +2895,7 @@ __global__ __launch_bounds__(64 * (1 + FZ_FRAMES)) void zd_k_fused(
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (mine && role == 0) FZT(f, 2);
   if (mine && role == 0) {
     if (rej) redo[f] = 1;
     *(volatile uint32_t*)&prog[q] = rej ? K4F_PROG_ABANDON : K4F_PROG_FINAL;
@@ -3783,8 +4034,11 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
       hipLaunchKernelGGL(zd_k_tables_huge, dim3(K1H_GRID), dim3(K1H_LANES), 0, st, a.src, a.src_size, comp, cstate,
                          fstate, (const uint32_t*)huge, luts);
   };
+  const bool fz = a.fused && !a.events;
   if (a.n_tables) {
-    if (fork) {
+    if (fz) {                                  // the sequence half runs in zd_k_fused
+      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
+    } else if (fork) {
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
       k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
     } else {
@@ -3822,15 +4076,15 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                          (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                          (const uint16_t*)fses, list);
   };
-  if (a.fused && !a.events) {
-    // K3 + K4 per group of four frames; K2 (forked) signals its workgroups;
+  if (fz) {
+    // K1's sequence half + K3 + K4 per group of four frames; K2 (forked) signals its workgroups;
     // then the redo pass for the frames the fused kernel flagged (normally none:
     // two launches whose workgroups exit at once)
     uint8_t* redo = ws + W.redo;
     const uint32_t k2need = fork ? (a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS : 0;
-    hipLaunchKernelGGL(zd_k_fused, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * (1 + FZ_FRAMES)), 0, s,
+    hipLaunchKernelGGL(zd_k_fused, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * FZ_WAVES), 0, s,
                        a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
-                       (const uint16_t*)fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
+                       fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, redo);
@@ -3868,6 +4122,15 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   return hipGetLastError();
 }
 
+#ifdef ZD_FZ_TRACE
+}  // namespace zd
+extern "C" int zd_debug_fz_trace(uint64_t* out, uint64_t* k2end) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zd::fz_tr), sizeof(zd::fz_tr), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(k2end, HIP_SYMBOL(zd::fz_k2end), 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return 0;
+}
+namespace zd {
+#endif
 #ifdef ZD_K1_PROF
 }  // namespace zd
 extern "C" int zd_debug_k1_prof(uint64_t out[8], int reset) {
