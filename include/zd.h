@@ -156,6 +156,12 @@ typedef struct zd_plan zd_plan;
  * keeps them as two launches.  Same output either way; tests run both. */
 #define ZD_F_NO_FUSE      32u
 
+/* zd_plan_info.executors: */
+#define ZD_EXEC_FUSED 1u   /* zd_k_fused: tables, FSE chains and execution per group of four
+                              single-block frames (not while kernel profiling is on) */
+#define ZD_EXEC_K4F   2u   /* some frames execute resident in LDS (zd_k_execute_lds) */
+#define ZD_EXEC_K4J   4u   /* some frames execute block-parallel (pointer jumping) */
+
 typedef struct zd_plan_info {
   uint64_t nframes;        /* frames in the plan (skippable included) */
   uint64_t nblocks;
@@ -167,7 +173,7 @@ typedef struct zd_plan_info {
   uint64_t nsequences;     /* sum of Number_of_Sequences over compressed blocks */
   uint64_t nliterals;      /* sum of Regenerated_Size over compressed-literal blocks */
   int32_t  index_status;   /* status of the host walk (first failing frame) */
-  uint32_t _pad;
+  uint32_t executors;      /* ZD_EXEC_* bits: the executors the plan's frames take */
   uint64_t host_ns;        /* zd_plan_create: header walk + descriptors (host work) */
   uint64_t device_ns;      /* zd_plan_create: workspace allocation + descriptor upload */
   uint64_t walk_serial_bytes; /* input bytes the frame walk had to walk serially (a range whose

@@ -20,17 +20,17 @@ plan = Plan(data)
 nf = plan.info.nframes
 d_src = torch.frombuffer(bytearray(data + bytes(64)), dtype=torch.uint8).cuda()
 d_dst = torch.empty(plan.info.out_bytes + 64, dtype=torch.uint8, device="cuda")
-buf = (C.c_uint64 * (1024 * 8))()
+buf = (C.c_uint64 * (1024 * 16))()
 k2 = C.c_uint64()
-names = ["start", "tables", "chain end", "K4 waits over", "K4 end", "chain start"]
+names = ["start", "tables", "chain end", "K4 waits over", "K4 end", "chain start", "parsed", "built", "K4 start", "parse start"]
 for it in range(4):
     plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), d_dst.numel())
     torch.cuda.synchronize()
     L.zd_debug_fz_trace(buf, C.byref(k2))
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:min(nf, 1024), :6].astype(np.int64)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:min(nf, 1024), :10].astype(np.int64)
     t0 = t[:, 0].min()
     us = (t - t0) / 100.0                     # s_memrealtime: 100 MHz
-    row = {names[i]: (round(float(np.median(us[:, i])), 1), round(float(us[:, i].max()), 1)) for i in range(6)}
+    row = {names[i]: (round(float(np.median(us[:, i])), 1), round(float(us[:, i].max()), 1)) for i in range(10)}
     k2us = (int(k2.value) - t0) / 100.0
     lag = us[:, 4] - us[:, 2]
     print(f"iter {it}: (median, max) us {row}; K2 end {k2us:.1f}; K4 end - chain end median {np.median(lag):.1f} max {lag.max():.1f}",

@@ -12,6 +12,6 @@ for i in 1 2; do
   python -c "import json;d=json.load(open('gpurun_out/r3fz5_c3_$i.json'));print(d['value'],d['ms_per_step'],d.get('verified_bit_exact'))"
 done
 ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_fztrace.so timeout -k 10 300 python scripts/fztrace.py > gpurun_out/fztrace5.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/fztrace5.log | tail -3; [ $rc = 0 ] || exit $rc
-ZD_FUZZ_SEED=731 ZD_FUZZ_ITERS=500 ZD_FUZZ_PLAN_ITERS=1500 timeout -k 10 600 \
-  python -u -m pytest tests/test_fuzz.py -v -s -p no:cacheprovider --timeout 550 --timeout-method thread > gpurun_out/fuzz_731.log 2>&1
-rc=$?; echo "fuzz rc=$rc: $(grep -i 'outcome' gpurun_out/fuzz_731.log | tr '\n' ' ' | cut -c1-400) $(tail -1 gpurun_out/fuzz_731.log)"
+ZD_FUZZ_SEED=732 ZD_FUZZ_ITERS=500 ZD_FUZZ_PLAN_ITERS=1500 timeout -k 10 600 \
+  python -u -m pytest tests/test_fuzz.py -v -s -p no:cacheprovider --timeout 550 --timeout-method thread > gpurun_out/fuzz_732.log 2>&1
+rc=$?; echo "fuzz rc=$rc: $(grep -i 'outcome' gpurun_out/fuzz_732.log | tr '\n' ' ' | cut -c1-400) $(tail -1 gpurun_out/fuzz_732.log)"

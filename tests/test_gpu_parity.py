@@ -341,6 +341,78 @@ def test_fused_plans():
                 assert_parity(bytes(d), False, f"flags={flags} {name} corrupt #{it}", flags=flags)
 
 
+def _random_probs(r, al, nsym):
+    """A random NCount distribution of nsym symbols summing to 1 << al in
+    absolute value, with "less than one" (-1) and zero probabilities."""
+    T = 1 << al
+    probs = [0] * nsym
+    rem = T
+    for i in r.sample(range(nsym), min(nsym, T)):
+        if rem == 0:
+            break
+        if r.random() < 0.2:
+            probs[i] = -1
+            rem -= 1
+    while rem > 0:
+        i = r.randrange(nsym)
+        if probs[i] >= 0:
+            k = min(rem, r.randint(1, max(1, rem // 4)))
+            probs[i] += k
+            rem -= k
+    while probs and probs[-1] == 0:                   # the description ends at its last nonzero
+        probs.pop()
+    return probs
+
+
+def _table_frame(r):
+    """One single-block frame whose sequence section exercises the table
+    builders: per table predefined, RLE or an FSE description (AL 5-9, up to
+    255 symbols, -1 probabilities), sometimes damaged (AL > 9, truncated, no
+    bitstream left); three raw literals and 1-5 sequences of random bits."""
+    modes, tables = 0, b""
+    for k, shift in enumerate((6, 4, 2)):              # LL, OF, ML
+        m = r.choice([0, 1, 2, 2])
+        modes |= m << shift
+        if m == 1:
+            tables += bytes([r.randrange(64) if r.random() < 0.9 else r.randrange(256)])
+        elif m == 2:
+            al = r.randint(5, 9)
+            nsym = r.choice([r.randint(2, 36), r.randint(2, 64), r.randint(65, 255)])
+            t = _ncount(al, _random_probs(r, al, nsym))
+            if r.random() < 0.05:
+                t = bytes([(t[0] & 0xF0) | 0x0F]) + t[1:]   # AL 20
+            tables += t
+    nseq = r.choice([1, 2, 5])
+    bitstream = b"" if r.random() < 0.05 else \
+        bytes(r.randrange(256) for _ in range(r.randrange(2, 16))) + bytes([r.randrange(1, 256)])
+    seqs = bytes([nseq, modes]) + tables + bitstream
+    if r.random() < 0.05:
+        seqs = seqs[: r.randrange(2, len(seqs))]          # truncated inside the descriptions
+    content = bytes([(3 << 3) | 0]) + b"xyz" + seqs
+    hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
+    return b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x00]) + hdr + content
+
+
+def test_fused_table_builds():
+    """zd_k_fused builds the sequence tables on its K4 waves (fz_tables,
+    fz_build_fse), not zd_k_tables: crafted frames (predefined / RLE / FSE
+    tables of AL 5-9 and up to 255 symbols, -1 probabilities, damaged
+    descriptions, deep OF tables for the redo pass) each decoded as the last
+    frame of a 300-frame plan, which takes the fused path, and on the
+    two-launch pipeline (ZD_F_NO_FUSE); status and output as the oracle's."""
+    from zstd_decompressor import _lib
+    r = random.Random(4242)
+    filler = gen.frames(gen.text(299 * 2048, seed=51), 2048, 3)
+    from zstd_decompressor.batch import Plan
+    for i in range(40):
+        data = filler + _table_frame(r)
+        plan = Plan(data)
+        assert plan.info.executors & _lib.EXEC_FUSED, "the 300-frame plan takes zd_k_fused"
+        plan.close()
+        for flags in (0, _lib.F_NO_FUSE):
+            assert_parity(data, False, f"table frame #{i} flags={flags}", flags=flags)
+
+
 def test_plan_decompress_reuses_the_plan(resources):
     """zd_plan_decompress: host in / host out with a plan made once (the
     INTEGRATION.md decompress() pattern), equal to the oracle's output."""

@@ -694,6 +694,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   I.nsequences = T.nseq;
   I.nliterals = T.lits;
   I.index_status = P->index_status;
+  I.executors = (P->fused ? ZD_EXEC_FUSED : 0u) | (P->n_k4f ? ZD_EXEC_K4F : 0u) | (P->n_jframes ? ZD_EXEC_K4J : 0u);
   return 0;
 }
 

@@ -142,6 +142,7 @@ struct FwBits {
     pos += len;
     return 0;
   }
+  __device__ inline void skip(int len) { pos += len; }
   __device__ inline uint32_t bytes_read() const { return pos / 8 + (pos % 8 > 0); }
 };
 
@@ -154,8 +155,53 @@ constexpr int K1_BIG = 1;
 constexpr int K1_HUGE = 2;
 constexpr uint32_t K1S_SYMS = 64;
 
+// ForwardBitParser over a wave's registers (zd_k_fused's K4 waves): dword i
+// from a 4-aligned base on lane i % 64 of r[i / 64]; FwBits' 64-bit cache
+// refilled by two readlanes instead of a dependent memory load (past the
+// 512 bytes held: memory).  The wave runs it on uniform values.
+struct FwBitsW {
+  const uint8_t* d;
+  uint32_t nbytes;
+  uint32_t pos;
+  uint32_t r0, r1;
+  uint32_t delta;                                  // bit of the register base where d starts
+  uint64_t cache = 0;
+  int64_t cbit = -1;                               // register-base bit of cache bit 0 (-1: empty)
+  __device__ inline uint32_t bits(uint32_t at, int len) {   // len <= 24, within range
+    const uint32_t a = at + delta;
+    if (cbit < 0 || (int64_t)a < cbit || (int64_t)a + len > cbit + 64) {
+      const uint32_t w = a >> 5;
+      if (w + 1 < 128) {
+        const uint32_t lo = (uint32_t)(w < 64 ? __builtin_amdgcn_readlane((int)r0, (int)w)
+                                              : __builtin_amdgcn_readlane((int)r1, (int)(w - 64)));
+        const uint32_t hi = (uint32_t)(w + 1 < 64 ? __builtin_amdgcn_readlane((int)r0, (int)(w + 1))
+                                                  : __builtin_amdgcn_readlane((int)r1, (int)(w - 63)));
+        cache = ((uint64_t)hi << 32) | lo;
+        cbit = (int64_t)w * 32;
+      } else {
+        cache = load_u64(d + (at >> 3), d, d + nbytes);
+        cbit = (int64_t)delta + (int64_t)(at >> 3) * 8;
+      }
+    }
+    return (uint32_t)(cache >> ((int64_t)a - cbit)) & ((1u << len) - 1);
+  }
+  __device__ inline int peek(int len, uint32_t* v) {
+    if ((int64_t)nbytes * 8 - pos < len) return ZD_E_NOT_ENOUGH_BITS;
+    *v = len ? bits(pos, len) : 0;
+    return 0;
+  }
+  __device__ inline int take(int len, uint32_t* v) {
+    if (int r = peek(len, v)) return r;
+    pos += len;
+    return 0;
+  }
+  __device__ inline void skip(int len) { pos += len; }
+  __device__ inline uint32_t bytes_read() const { return pos / 8 + (pos % 8 > 0); }
+};
+
 // parse_fse_table (fse.rs:16-69); dist holds max_sym entries (256: all)
-__device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t* nsym_out, uint32_t max_sym) {
+template <typename BR>
+__device__ int parse_ncount(BR& in, uint8_t* al_out, int16_t* dist, uint32_t* nsym_out, uint32_t max_sym) {
   uint32_t v;
   if (int r = in.take(4, &v)) return r;
   int al = (int)v + 5;
@@ -166,19 +212,15 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
     int bits = highbit32((uint32_t)remaining + 1) + 1;
     uint32_t pk;
     if (int r = in.peek(bits, &pk)) return r;
-    uint32_t lower_mask = (1u << (bits - 1)) - 1;
-    uint32_t threshold = (1u << bits) - 1 - ((uint32_t)remaining + 1);
-    int32_t decoded;
-    if ((pk & lower_mask) < threshold) {
-      if (int r = in.take(bits - 1, &v)) return r;
-      decoded = (int32_t)v;
-    } else if (pk > lower_mask) {
-      if (int r = in.take(bits, &v)) return r;
-      decoded = (int32_t)v - (int32_t)threshold;
-    } else {
-      if (int r = in.take(bits, &v)) return r;
-      decoded = (int32_t)v;
-    }
+    const uint32_t lower_mask = (1u << (bits - 1)) - 1;
+    const uint32_t threshold = (1u << bits) - 1 - ((uint32_t)remaining + 1);
+    // the reference's take(bits - 1) reads pk's low bits, take(bits) pk: one
+    // read (the peek's bound covers both)
+    const uint32_t low = pk & lower_mask;
+    const bool short_code = low < threshold;
+    const int32_t decoded = short_code ? (int32_t)low
+                                       : (pk > lower_mask ? (int32_t)pk - (int32_t)threshold : (int32_t)pk);
+    in.skip(short_code ? bits - 1 : bits);
     int32_t proba = decoded - 1;
     remaining -= proba < 0 ? -proba : proba;
     if (n_sym < max_sym) dist[n_sym] = (int16_t)proba;
@@ -210,9 +252,10 @@ __device__ int parse_ncount(FwBits& in, uint8_t* al_out, int16_t* dist, uint32_t
 #ifdef ZD_FZ_TRACE
 // zd_k_fused timeline (scripts/fztrace.py): per frame s_memrealtime at the
 // kernel's start, tables ready, chain end, K4's waits over, K4 end; K2's end
-__device__ uint64_t fz_tr[1024][8];
+__device__ uint64_t fz_tr[1024][16];
 __device__ uint64_t fz_k2end;
 #define FZT(f, i) do { if ((f) < 1024) fz_tr[f][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define FZT_ON 1
 #else
 #define FZT(f, i) do { } while (0)
 #endif
@@ -1594,9 +1637,6 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
-#ifndef ZD_FZ_PUB
-#define ZD_FZ_PUB 16                 // records between publications (a multiple of 16)
-#endif
 template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
@@ -1676,7 +1716,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
       outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
       if constexpr (PUB) {
-        if (((slot + 2) & (ZD_FZ_PUB - 1)) == 0 && slot + 2 >= 32) {
+        if (((slot + 2) & 15) == 0 && slot + 2 >= 32) {
           asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
           if (role == 0) *prog = (slot + 2 - 16) >> 4;
         }
@@ -2600,7 +2640,6 @@ struct FzInfo {                      // a block's table results, for wave 0
   uint32_t err;                      // first failure: sub << 8 | -code (0: none)
   uint32_t bo, bsz;                  // sequence bitstream
 };
-constexpr uint32_t FZ_DESC = 2048;   // description bytes staged in LDS (three tables need <= ~1.3 KB)
 
 __device__ inline uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -2662,70 +2701,75 @@ __device__ int fz_build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t
   for (uint32_t i0 = 0; i0 < T; i0 += 64) {
     const uint32_t i = i0 + lane;
     const uint32_t s = i < T ? W.sym[i] : 0u;
+    // the lane's rank among the chunk's states of its symbol, and their
+    // number (registers only: one round per distinct symbol)
     uint64_t rem = __ballot(i < T);
-    uint32_t ns = 0;
+    uint32_t occ = 0, tot = 0;
     while (rem) {
       const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)__builtin_ctzll(rem));
       const uint64_t m = __ballot(s == sl) & rem;
-      const uint32_t base = W.cnt[sl];
-      if ((m >> lane) & 1) ns = base + lanes_below(m);
-      k4_sync();
-      if (lane == 0) W.cnt[sl] = (uint16_t)(base + (uint32_t)__popcll(m));
-      k4_sync();
+      if ((m >> lane) & 1) { occ = lanes_below(m); tot = (uint32_t)__popcll(m); }
       rem &= ~m;
     }
+    const uint32_t ns = i < T ? W.cnt[s] + occ : 0u;
+    k4_sync();
+    if (i < T && occ + 1 == tot) W.cnt[s] = (uint16_t)(ns + 1);   // the symbol's last state in the chunk
+    k4_sync();
     if (i < T) tab[i] = fse_entry(s, ns);
   }
   k4_sync();
   return 0;
 }
 
-// A K4 wave's block: k1_sequences_lane's walk (sequences.rs:91-187) with the
-// descriptions parsed by lane 0 from an LDS copy and each table built by the
-// wave; then what zd_k_tables leaves (the tables the serial walk completes
+// A K4 wave's block: k1_sequences_lane's walk (sequences.rs:91-187), each
+// table built by the wave; then what zd_k_tables leaves (the tables the serial walk completes
 // in the block's slot, their accuracy logs, the bitstream, a parse error's
 // key), the K3 tables for wave 0 (tabs, when they fit) and the block's
 // FzInfo.  Every lane returns.
 __device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* __restrict__ src, const CompBlock& C, uint32_t ci, CompState* cstate,
-                          FrameState* fstate, uint16_t* fses, FzK1& W, l_u8* desc, lds_u16* k3tab, FzInfo& I,
-                          int lane) {
-  // the description bytes (<= FZ_DESC: NCount descriptions of <= 255
-  // symbols of <= 10 bits each take <= 410 bytes, the RLE bytes one)
+                          FrameState* fstate, uint16_t* fses, FzK1& W, lds_u16* k3tab, FzInfo& I, int lane,
+                          uint32_t f) {
+  // the descriptions in order, by every lane on the same (wave-uniform)
+  // values, so the walk runs on the scalar unit: one lane of a wave64 would
+  // take four cycles an operation (0.03 ms for a block's three tables)
   const uint32_t base = C.seq_tables;
-  const uint32_t avail = C.size > base ? C.size - base : 0u;
-  const uint32_t ncopy = avail < FZ_DESC ? avail : FZ_DESC;
-  for (uint32_t x = lane; x < ncopy; x += 64) desc[x] = src[C.src + base + x];
-  k4_sync();
-  // lane 0: the descriptions in order; results by readlane
+  const uint8_t* blk = src + C.src;
+  // the description bytes in registers (512 from a 4-aligned base; a dword
+  // that starts past the block reads as 0, none reaches past the input)
+  const uint8_t* wb = (const uint8_t*)((uintptr_t)(blk + base) & ~(uintptr_t)3);
+  const uint8_t* bend = blk + C.size;
+  const uint32_t r0 = wb + 4 * lane < bend ? *(const uint32_t*)(wb + 4 * lane) : 0u;
+  const uint32_t r1 = wb + 4 * (lane + 64) < bend ? *(const uint32_t*)(wb + 4 * (lane + 64)) : 0u;
+#ifdef FZT_ON
+  if (lane == 0) FZT(f, 9);
+#endif
   int pst = 0, psub = 3;
   uint32_t alp = 0, nsp = 0, rle = 0, pos = base;
-  if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      if (pst) break;
-      const int mode = C.modes[k];
-      int st = 0, al = 0;
-      uint32_t nsym = 0;
-      if (mode == M_RLE) {
-        if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
-        else { rle |= (uint32_t)desc[pos - base] << (8 * k); pos++; }
-      } else if (mode == M_FSE) {
-        if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
-        else {
-          FwBits fw{(const uint8_t*)(desc + (pos - base)), C.size - pos, 0};
-          uint8_t a = 0;
-          st = parse_ncount(fw, &a, W.dist[k], &nsym, 256);
-          al = a;
-          pos += fw.bytes_read();
-        }
-      } else if (mode == M_PREDEFINED) {
-        al = k == 1 ? 5 : 6;
-        nsym = k == 0 ? 36 : (k == 1 ? 29 : 53);
+  for (int k = 0; k < 3; k++) {
+    if (pst) break;
+    const int mode = C.modes[k];
+    int st = 0, al = 0;
+    uint32_t nsym = 0;
+    if (mode == M_RLE) {
+      if (pos >= C.size) st = ZD_E_NOT_ENOUGH_BYTES;
+      else { rle |= (uint32_t)blk[pos] << (8 * k); pos++; }
+    } else if (mode == M_FSE) {
+      if (pos >= C.size) st = ZD_E_EMPTY_SLICE;
+      else {
+        FwBitsW fw{blk + pos, C.size - pos, 0, r0, r1, (uint32_t)(8 * (blk + pos - wb))};
+        uint8_t a = 0;
+        st = parse_ncount(fw, &a, W.dist[k], &nsym, 256);
+        al = a;
+        pos += fw.bytes_read();
       }
-      if (st) { pst = st; psub = k; }
-      alp |= (uint32_t)al << (8 * k);
-      nsp |= nsym << (9 * k);
+    } else if (mode == M_PREDEFINED) {
+      al = k == 1 ? 5 : 6;
+      nsym = k == 0 ? 36 : (k == 1 ? 29 : 53);
     }
+    if (st) { pst = st; psub = k; }
+    alp |= (uint32_t)al << (8 * k);
+    nsp |= nsym << (9 * k);
   }
   pst = __builtin_amdgcn_readfirstlane(pst);
   psub = __builtin_amdgcn_readfirstlane(psub);
@@ -2734,6 +2778,7 @@ __device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* _
   rle = (uint32_t)__builtin_amdgcn_readfirstlane((int)rle);
   pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
   k4_sync();
+  if (lane == 0) FZT(f, 6);
   // the tables before the first parse failure, in order; a build failure
   // stops the walk there
   int fst = pst, fsub = pst ? psub : 4;
@@ -2757,6 +2802,7 @@ __device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* _
     if (st) { fst = st; fsub = k; break; }
   }
   k4_sync();
+  if (lane == 0) FZT(f, 7);
   if (!fst && pos >= C.size) { fst = ZD_E_EMPTY_SLICE; fsub = 3; }   // seq.bitstream of the empty rest
   const uint32_t bo = fsub >= 3 ? pos : 0u;
   const uint32_t bsz = fsub >= 3 && pos < C.size ? C.size - pos : 0u;
@@ -2787,14 +2833,10 @@ __device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* _
   }
 }
 
-#ifndef ZD_FZ_SOLO
-#define ZD_FZ_SOLO 0                 // 1: eight waves, K4 frames on waves 1-3 and 5-7 (wave 4 idle)
-#endif
-#ifndef ZD_FZ_PRIO
-#define ZD_FZ_PRIO 0                 // the chain wave's s_setprio
-#endif
-constexpr int FZ_FRAMES = ZD_FZ_SOLO ? 6 : 4;
-constexpr int FZ_WAVES = ZD_FZ_SOLO ? 8 : 1 + FZ_FRAMES;
+// (measured on C3, within noise: the chain wave at s_setprio 3; eight waves
+// so the chain wave has a SIMD to itself; publishing every 32 records)
+constexpr int FZ_FRAMES = 4;
+constexpr int FZ_WAVES = 1 + FZ_FRAMES;
 __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
     const uint8_t* __restrict__ src, uint8_t* outbase, const FrameDesc* __restrict__ frames, FrameState* fstate,
     const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp, CompState* cstate,
@@ -2809,15 +2851,16 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
   __shared__ uint32_t prog[FZ_FRAMES], trdy[FZ_FRAMES];
   __shared__ __attribute__((aligned(16))) FzK1 k1w[FZ_FRAMES];
   __shared__ FzInfo info[FZ_FRAMES];
-  static_assert(FZ_DESC <= K4_C, "the description copy lives in the K4 window");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (threadIdx.x < FZ_FRAMES) prog[threadIdx.x] = trdy[threadIdx.x] = 0;
   __syncthreads();
   if (wave > 0) {
-    if (ZD_FZ_SOLO && (wave & 3) == 0) return;
-    const int q = ZD_FZ_SOLO ? wave - 1 - (wave >> 2) : wave - 1;
+    // (readfirstlane: the compiler sees the frame as wave-uniform, so the
+    // table walk below runs on the scalar unit)
+    const int q = __builtin_amdgcn_readfirstlane(wave - 1);
     const uint32_t f = blockIdx.x * FZ_FRAMES + q;
     if (f >= n_frames) return;
+    if (lane == 0) FZT(f, 8);
     {
       // the block's sequence tables (the window is free until the waits)
       const FrameDesc F = frames[f];
@@ -2829,8 +2872,7 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
         build = C.nseq > 0 && C.host_stage > PS_SEQ_TABLES && !C.prebuilt;
       }
       if (build) {
-        fz_tables(src, C, (uint32_t)c, cstate, fstate, fses, k1w[q], (l_u8*)win[q], (lds_u16*)tabs + q * K3_TAB,
-                  info[q], lane);
+        fz_tables(src, C, (uint32_t)c, cstate, fstate, fses, k1w[q], (lds_u16*)tabs + q * K3_TAB, info[q], lane, f);
       } else if (lane == 0) {
         info[q] = FzInfo{0u, 0u, 0u, 0u};
       }
@@ -2849,7 +2891,6 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
     return;
   }
   // wave 0: the chains (quad q: frame blockIdx.x * FZ_FRAMES + q)
-  if (ZD_FZ_PRIO) __builtin_amdgcn_s_setprio(ZD_FZ_PRIO);
   const int role = lane & 3, q = lane >> 2;
   const uint32_t f = blockIdx.x * FZ_FRAMES + q;
   const bool mine = q < FZ_FRAMES && f < n_frames;

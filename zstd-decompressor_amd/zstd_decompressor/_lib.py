@@ -42,7 +42,7 @@ class PlanInfo(C.Structure):
     _fields_ = [("nframes", C.c_uint64), ("nblocks", C.c_uint64), ("ncompressed", C.c_uint64),
                 ("src_bytes", C.c_uint64), ("out_bytes", C.c_uint64), ("out_exact", C.c_uint64),
                 ("workspace_bytes", C.c_uint64), ("nsequences", C.c_uint64), ("nliterals", C.c_uint64),
-                ("index_status", C.c_int32), ("_pad", C.c_uint32), ("host_ns", C.c_uint64),
+                ("index_status", C.c_int32), ("executors", C.c_uint32), ("host_ns", C.c_uint64),
                 ("device_ns", C.c_uint64), ("walk_serial_bytes", C.c_uint64),
                 ("io_h2d_ns", C.c_uint64), ("io_decode_ns", C.c_uint64), ("io_d2h_ns", C.c_uint64),
                 ("error_key", C.c_uint64), ("replans", C.c_uint64)]
@@ -177,3 +177,4 @@ F_BLOCK_PARALLEL = 2   # every frame with a compressed block -> K4J (block-paral
 F_FRAME_SERIAL = 4     # no frame -> K4J
 F_SEQ_ONE_LANE = 8     # K3 one lane per block instead of four (K3Q)
 F_NO_FUSE = 32         # K3 then K4 as two launches in few-frame plans (no zd_k_fused)
+EXEC_FUSED, EXEC_K4F, EXEC_K4J = 1, 2, 4   # zd_plan_info.executors bits (include/zd.h ZD_EXEC_*)
