@@ -155,6 +155,10 @@ typedef struct zd_plan zd_plan;
  * K3 and K4 run fused per frame group (zd_k_fused) by default; this flag
  * keeps them as two launches.  Same output either way; tests run both. */
 #define ZD_F_NO_FUSE      32u
+/* Table-build choice for plans of up to 8,192 tables: K1's sequence half
+ * runs one wave per block by default; this flag keeps K1's serial lanes.
+ * Same tables either way; tests run both. */
+#define ZD_F_K1_LANES     64u
 
 /* zd_plan_info.executors: */
 #define ZD_EXEC_FUSED 1u   /* zd_k_fused: tables, FSE chains and execution per group of four

@@ -59,7 +59,10 @@ def _dump_ood(data, p, tag):
 
 
 def test_fuzz_structure_aware():
-    """ZD_FUZZ_ITERS / ZD_FUZZ_SEED run longer campaigns (default: 600 inputs)."""
+    """ZD_FUZZ_ITERS / ZD_FUZZ_SEED run longer campaigns (default: 600 inputs).
+    A quarter of the inputs build their tables on K1's lanes (ZD_F_K1_LANES),
+    the rest on the wave-per-block build of small plans."""
+    from zstd_decompressor import _lib
     from zstd_decompressor.batch import decompress_status
     iters = int(os.environ.get("ZD_FUZZ_ITERS", "600"))
     r = random.Random(int(os.environ.get("ZD_FUZZ_SEED", str(0xF022)), 0))
@@ -68,8 +71,9 @@ def test_fuzz_structure_aware():
     for it in range(iters):
         data = _mutate(r, seeds)
         p = r.random() < 0.3
+        flags = _lib.F_K1_LANES if r.random() < 0.25 else 0
         ost, oout = oracle.decompress_status(data, p)
-        gst, gout = decompress_status(data, p)
+        gst, gout = decompress_status(data, p, flags)
         if gst == OUT_OF_DOMAIN:
             seen["ood"] += 1
             _dump_ood(data, p, f"s{it}")

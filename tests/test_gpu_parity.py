@@ -399,7 +399,8 @@ def test_fused_table_builds():
     tables of AL 5-9 and up to 255 symbols, -1 probabilities, damaged
     descriptions, deep OF tables for the redo pass) each decoded as the last
     frame of a 300-frame plan, which takes the fused path, and on the
-    two-launch pipeline (ZD_F_NO_FUSE); status and output as the oracle's."""
+    two-launch pipeline (ZD_F_NO_FUSE: zd_k_tables_seqw, and with
+    ZD_F_K1_LANES K1's lanes); status and output as the oracle's."""
     from zstd_decompressor import _lib
     r = random.Random(4242)
     filler = gen.frames(gen.text(299 * 2048, seed=51), 2048, 3)
@@ -409,7 +410,7 @@ def test_fused_table_builds():
         plan = Plan(data)
         assert plan.info.executors & _lib.EXEC_FUSED, "the 300-frame plan takes zd_k_fused"
         plan.close()
-        for flags in (0, _lib.F_NO_FUSE):
+        for flags in (0, _lib.F_NO_FUSE, _lib.F_NO_FUSE | _lib.F_K1_LANES):
             assert_parity(data, False, f"table frame #{i} flags={flags}", flags=flags)
 
 
@@ -494,7 +495,10 @@ def _ncount(al, probs):
 def test_k1_large_tables():
     """Sequence tables with more than 64 symbols (LL codes past the maximum):
     K1's first pass flags the block and the large-scratch pass builds it
-    (zd_kernels.hip zd_k_tables<true>); status and output match the oracle."""
+    (zd_kernels.hip zd_k_tables<true>, under ZD_F_K1_LANES), or the
+    wave-per-block build does (zd_k_tables_seqw, the default for small
+    plans); status and output match the oracle."""
+    from zstd_decompressor import _lib
     r = random.Random(77)
     for nsym, al in ((70, 6), (65, 7), (100, 7), (255, 8)):
         probs = [1] * (nsym - 1) + [(1 << al) - (nsym - 1)]   # the last symbol takes the rest
@@ -510,7 +514,8 @@ def test_k1_large_tables():
             content = lits + seqs
             hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
             frame = b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x00]) + hdr + content
-            assert_parity(frame, False, f"nsym {nsym} al {al} trial {trial}")
+            for flags in (0, _lib.F_K1_LANES):
+                assert_parity(frame, False, f"nsym {nsym} al {al} trial {trial} flags {flags}", flags=flags)
 
 
 def _deep_tree_frame(r, nbytes, weights=None):

@@ -2818,7 +2818,7 @@ __device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* _
     for (int e = lane; e < cnt; e += 64) {
       const uint32_t v = W.tab[k][e];
       g[e] = (uint16_t)v;
-      if (cnt <= cap[k]) k3tab[dst[k] + e] = (uint16_t)K3_ENTRY(v, k, al);
+      if (k3tab && cnt <= cap[k]) k3tab[dst[k] + e] = (uint16_t)K3_ENTRY(v, k, al);
     }
     if (lane == 0) cstate[ci].al[k] = (uint8_t)al;
   }
@@ -2831,6 +2831,22 @@ __device__ __attribute__((always_inline)) inline void fz_tables(const uint8_t* _
     I.bo = bo;
     I.bsz = bsz;
   }
+}
+
+// K1's sequence half for plans of few blocks (zd_k_tables PART 2 there is
+// one round of serial lanes, 0.25 ms for C3's 763 blocks): one wave per
+// block, fz_tables' walk and wave-parallel builds, the same slot, CompState
+// bytes and keys.
+__global__ __launch_bounds__(64) void zd_k_tables_seqw(const uint8_t* __restrict__ src,
+                                                       const CompBlock* __restrict__ comp, CompState* cstate,
+                                                       FrameState* fstate, const uint32_t* __restrict__ list,
+                                                       uint32_t n_list, uint16_t* fses) {
+  __shared__ __attribute__((aligned(16))) FzK1 W;
+  __shared__ FzInfo I;
+  const uint32_t ci = (uint32_t)__builtin_amdgcn_readfirstlane((int)list[blockIdx.x]);
+  const CompBlock C = comp[ci];
+  if (C.prebuilt || C.nseq == 0 || C.host_stage <= PS_SEQ_TABLES) return;
+  fz_tables(src, C, ci, cstate, fstate, fses, W, nullptr, I, (int)threadIdx.x, C.frame);
 }
 
 // (measured on C3, within noise: the chain wave at s_setprio 3; eight waves
@@ -4076,9 +4092,16 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                          fstate, (const uint32_t*)huge, luts);
   };
   const bool fz = a.fused && !a.events;
+  auto k1seqw = [&](hipStream_t st) {
+    hipLaunchKernelGGL(zd_k_tables_seqw, dim3(a.n_tables), dim3(64), 0, st, a.src, comp, cstate, fstate,
+                       (const uint32_t*)(ws + W.list_tables), a.n_tables, fses);
+  };
   if (a.n_tables) {
     if (fz) {                                  // the sequence half runs in zd_k_fused
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
+    } else if (a.k1_seq_waves) {               // few blocks: the sequence half one wave per block
+      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
+      k1seqw(s);
     } else if (fork) {
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
       k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
@@ -4155,9 +4178,13 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, (const JSeg*)jseg, jsd, jst);
     const uint64_t gw = (a.j_pieces + 255) / 256;
     const dim3 gr((uint32_t)(gw < 8192 ? (gw + 7) & ~7ull : 8192));   // a multiple of 8 (one eighth per XCD)
+    // rounds past the second with a smaller grid (it strides over every
+    // piece): they are the deepest chains' tail, usually empty, and an
+    // empty round then costs little more than its launch
+    const dim3 gt(std::min<uint32_t>(gr.x, 1024u));
     for (uint32_t r = 1; r <= a.j_rounds; r++)
-      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes, a.j_pieces,
-                         jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == a.j_rounds));
+      hipLaunchKernelGGL(zd_k_jround, r <= 2 ? gr : gt, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
+                         a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == a.j_rounds));
   }
   if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;
   return hipGetLastError();
