@@ -155,7 +155,7 @@ typedef struct zd_plan zd_plan;
  * K3 and K4 run fused per frame group (zd_k_fused) by default; this flag
  * keeps them as two launches.  Same output either way; tests run both. */
 #define ZD_F_NO_FUSE      32u
-/* Table-build choice for plans of up to 8,192 tables: K1's sequence half
+/* Table-build choice for plans of up to 16,384 tables: K1's sequence half
  * runs one wave per block by default; this flag keeps K1's serial lanes.
  * Same tables either way; tests run both. */
 #define ZD_F_K1_LANES     64u

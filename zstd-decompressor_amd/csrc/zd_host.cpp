@@ -489,7 +489,10 @@ size_t k3_slots() {
 // workgroup per CU, so K2's workgroups (which the fused K4 waves wait for)
 // always find room beside them.  ZD_FUSE=0/1 forces it off/on where allowed.
 constexpr size_t FUSE_MIN_FRAMES = 256;
-constexpr uint64_t K1W_MAX_BLOCKS = 8192;
+// zd_k_tables_seqw up to this many tables (scripts/r3_k1wmax.sh, bench value
+// lanes -> waves: one rank's C4 share at 8 GPUs, 10,240 blocks, 237 -> 241 and
+// 234 -> 237 GB/s; full C4, 81,920 blocks, 274 -> 270)
+constexpr uint64_t K1W_MAX_BLOCKS = 16384;
 bool fuse_plan(const zd_plan* P, uint64_t out_len0) {
   static const char* env = getenv("ZD_FUSE");
   if (env && atoi(env) == 0) return false;
@@ -1590,10 +1593,12 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   static const char* fork_env = getenv("ZD_FORK");
   const bool fork = fork_env ? atoi(fork_env) == 1 : fork_auto(P->n_seq);
   if (fork) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
-  // K1's sequence half one wave per block where K1's lanes would run one
-  // round (C3 with ZD_F_NO_FUSE / c3s, 763 blocks: 0.25 -> 0.06 ms); the plan
-  // flag ZD_F_K1_LANES keeps the lanes
-  a.k1_seq_waves = P->n_tables <= K1W_MAX_BLOCKS && !(P->flags & ZD_F_K1_LANES);
+  // K1's sequence half one wave per block in plans of few tables (C3 with
+  // ZD_F_NO_FUSE / c3s, 763 blocks: 0.25 -> 0.06 ms); the plan flag
+  // ZD_F_K1_LANES keeps the lanes, ZD_K1W_MAX (read once) moves the bound
+  static const char* k1w_env = getenv("ZD_K1W_MAX");   // (read once) the block-count bound
+  const uint64_t k1w_max = k1w_env ? (uint64_t)atoll(k1w_env) : K1W_MAX_BLOCKS;
+  a.k1_seq_waves = P->n_tables <= k1w_max && !(P->flags & ZD_F_K1_LANES);
   if (P->fused && !P->profile) {
     a.fused = true;
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.redo, 0, std::max<uint64_t>(P->n_frames, 1), s));
