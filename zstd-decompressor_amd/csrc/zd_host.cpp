@@ -1593,6 +1593,13 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   static const char* fork_env = getenv("ZD_FORK");
   const bool fork = fork_env ? atoi(fork_env) == 1 : fork_auto(P->n_seq);
   if (fork) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
+  // no fork: K1's Huffman half on the second stream beside its sequence
+  // half, joined before K2 (ZD_K1FORK=0 / 1, read once)
+  static const char* k1f_env = getenv("ZD_K1FORK");
+  if (!fork && !P->profile && P->n_huf && P->n_seq && (k1f_env ? atoi(k1f_env) == 1 : true)) {
+    a.aux = P->aux; a.fork = P->fork; a.join = P->join;
+    a.k1_fork = true;
+  }
   // K1's sequence half one wave per block in plans of few tables (C3 with
   // ZD_F_NO_FUSE / c3s, 763 blocks: 0.25 -> 0.06 ms); the plan flag
   // ZD_F_K1_LANES keeps the lanes, ZD_K1W_MAX (read once) moves the bound

@@ -4073,9 +4073,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   // K2 and K3 are independent once their tables exist: with the fork, K1's
   // Huffman half and K2 run on the aux stream beside K1's sequence half and
   // K3 (not when timing kernels one by one)
-  const bool fork = a.aux && !a.events && a.n_huf && a.n_seq;
+  const bool fork = a.aux && !a.k1_fork && !a.events && a.n_huf && a.n_seq;
+  // without it, K1's two halves may still run on the two streams (joined
+  // before K2)
+  const bool k1f = a.aux && a.k1_fork && !a.events && a.n_tables;
   hipStream_t s2 = fork ? a.aux : s;
-  if (fork) {
+  if (fork || k1f) {
     if ((e = hipEventRecord(a.fork, s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(a.aux, a.fork, 0)) != hipSuccess) return e;
   }
@@ -4100,16 +4103,20 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     if (fz) {                                  // the sequence half runs in zd_k_fused
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
     } else if (a.k1_seq_waves) {               // few blocks: the sequence half one wave per block
-      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
+      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, k1f ? a.aux : s2, true);
       k1seqw(s);
-    } else if (fork) {
-      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
+    } else if (fork || k1f) {
+      k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, k1f ? a.aux : s2, true);
       k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
     } else {
       k1(zd_k_tables<false, 3>, zd_k_tables<true, 3>, s, true);
     }
   }
   if (a.events) if ((e = hipEventRecord(a.events[2], s)) != hipSuccess) return e;
+  if (k1f) {
+    if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
+  }
   if (a.n_huf)
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s2, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits,

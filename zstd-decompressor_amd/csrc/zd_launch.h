@@ -25,6 +25,7 @@ struct LaunchArgs {
   uint32_t j_hops = 8;                     // K4J: hops per pending word and round (ZD_J_HOPS)
   bool fused = false;                      // K3 + K4 as zd_k_fused, then the redo pass
   bool k1_seq_waves = false;               // K1's sequence half one wave per block (zd_k_tables_seqw)
+  bool k1_fork = false;                    // no K2 | K3 fork: K1's halves on the two streams (aux, fork, join)
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
