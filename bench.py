@@ -411,21 +411,13 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     ms_per_step = float(elapsed.item()) / args.steps
 
-    # ---- per-kernel times (events between launches on the same stream) ----
-    plan.set_profiling(True)
-    kt = {}
-    for _ in range(max(2, min(args.steps, 3))):
-        step()
-        for k, v in plan.kernel_times().items():
-            kt.setdefault(k, []).append(v)
-    plan.set_profiling(False)
-    kt = {k: float(np.mean(v)) for k, v in kt.items()}
-    dom = max(kt, key=kt.get)
-
-    # ---- verify (outside timing) ----
+    # ---- verify (outside timing): d_dst as the last timed step left it ----
+    # (the timed configuration itself: fused kernel, K2 | K3 fork and all;
+    # the profiled passes below run after this check)
     verified = None
+    st, total, _, _, _ = plan.results(d_dst.data_ptr(), sptr)
+    redo_frames = int(plan.refresh_info().fused_redo_frames)
     if not args.no_verify and src is not None:
-        st, total, _, _, _ = plan.results(d_dst.data_ptr(), sptr)
         ok = st == 0 and total == info.out_bytes
         if strong:
             ref = torch.frombuffer(bytearray(ref_bytes), dtype=torch.uint8).to(dev)
@@ -443,6 +435,29 @@ def main():
             dist.all_reduce(v, op=dist.ReduceOp.MIN)
             verified = bool(v.item())
         assert args.experiment or verified, "GPU output differs from the source bytes"
+
+    # ---- the dominant launch of the timed pipeline, as it runs (events on the
+    # plan's stream around zd_k_fused / zd_k_execute; fork and fusion kept) ----
+    nprof = max(2, min(args.steps, 3))
+    plan.set_profiling(2)
+    dts = []
+    for _ in range(nprof):
+        step()
+        dts.append(plan.kernel_times())
+    plan.set_profiling(0)
+    dom = next(iter(dts[0]))
+    dom_ms = float(np.mean([d[dom] for d in dts]))
+
+    # ---- per-kernel breakdown (events between launches on the same stream:
+    # the launches one after another, no fork, no fused kernel) ----
+    plan.set_profiling(True)
+    kt = {}
+    for _ in range(nprof):
+        step()
+        for k, v in plan.kernel_times().items():
+            kt.setdefault(k, []).append(v)
+    plan.set_profiling(False)
+    kt = {k: float(np.mean(v)) for k, v in kt.items()}
 
     # ---- gather of the decoded ranges to rank 0 over RCCL (never part of value) ----
     out_bytes = info.out_bytes
@@ -500,7 +515,6 @@ def main():
 
     value = total_out.item() / (ms_per_step / 1e3) / 1e6
     alg_per_launch = out_bytes + comp_bytes          # C + D, this rank's launch
-    dom_ms = kt[dom]
     achieved = alg_per_launch / (dom_ms / 1e3) / 1e9
 
     cpu = cpu_zstd = None
@@ -547,11 +561,17 @@ def main():
                 "decompressed_bytes_rank0": int(out_bytes),
                 "compressed_bytes_rank0": int(comp_bytes),
                 "sequences_rank0": int(info.nsequences),
+                "compression_ratio": round(out_bytes / max(comp_bytes, 1), 3),
+                "fidelity_note": "synthetic corpus (no enwik/Silesia offline): it compresses at compression_ratio, "
+                                 "real enwik text at ~3.5-4x at these levels (SURVEY.md Appendix A), so each output "
+                                 "byte here carries more sequences and literals than enwik9's would; value and "
+                                 "roofline.frac are not directly comparable to a real-enwik run",
                 "parallelism": f"frame-sharded x{world}" if strong else f"replicas x{world}",
             },
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,
+                "kernel_ms": round(dom_ms, 3),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -565,6 +585,10 @@ def main():
                 "pipeline_frac": round(alg_per_launch / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
+            "kernel_ms_note": "kernel_ms: a profiled pass with the launches one after another (no K2 | K3 fork, "
+                              "no fused kernel); roofline.kernel_ms: the dominant launch of the timed pipeline "
+                              "as it runs (HIP events on its stream around it)",
+            "fused_redo_frames": redo_frames,
             "host_plan_ms": round(host_plan_s * 1e3, 1),
             "host_plan_first_ms": round(host_plan_first_s * 1e3, 1),
             "device_walk_plan_ms": None if dev_plan_ms is None else round(dev_plan_ms, 1),

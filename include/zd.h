@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 6
+#define ZD_ABI_VERSION 7
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -191,7 +191,23 @@ typedef struct zd_plan_info {
                               csrc/zd_common.h); all ones when every frame decoded */
   uint64_t replans;        /* the last zd_plan_decompress: re-plans past frames that overran
                               their reserved capacity (or K4J rounds), 0 normally */
+  uint64_t fused_redo_frames; /* the last zd_plan_results of a zd_k_fused launch: frames its redo
+                              pass decoded (a fast-chain reject, or a wait for K2 / the chain
+                              past its bound); 0 normally, never a different output */
 } zd_plan_info;
+
+/* The executor routing zd_plan_create / zd_decode_async choose for a plan of
+ * this shape on a device of `cus` compute units (host only: diagnostics and
+ * tests).  Every bound scales with the CU count (zd_host.cpp route_plan,
+ * DESIGN.md §4): single_block_frames = every frame one compressed block.
+ * *route = ZD_ROUTE_* bits. */
+#define ZD_ROUTE_FUSED        1u   /* zd_k_fused (tables + K3 + K4 per group of four frames) */
+#define ZD_ROUTE_K4F          2u   /* frames up to 128 KiB execute resident in LDS */
+#define ZD_ROUTE_K1_SEQ_WAVES 4u   /* K1's sequence half one wave per block */
+#define ZD_ROUTE_FORK         8u   /* K2 beside K3 on a second stream */
+#define ZD_ROUTE_K1_FORK     16u   /* K1's two halves on the two streams */
+int zd_route(uint32_t cus, uint64_t nframes, uint64_t n_tables, uint64_t n_seq_blocks, uint64_t n_huf_blocks,
+             int single_block_frames, uint32_t flags, uint32_t* route);
 
 /* Index src[0..n) on the host and allocate the plan's device workspace.
  * Host-side work only (no kernel launches).  A frame that fails to index
@@ -246,9 +262,12 @@ int zd_plan_results(zd_plan* plan, uint8_t* d_dst, void* stream,
  * plan nframes entries, either may be NULL. */
 int zd_plan_checksums(zd_plan* plan, const uint8_t* d_dst, void* stream, int32_t* ok, uint64_t* hash);
 
-/* Per-kernel time of the last zd_decode_async on the plan, in ms (HIP
- * events recorded between launches when ZD_PROFILE_KERNELS was requested
- * through zd_plan_set_profiling).  names/ms arrays of cap entries. */
+/* Kernel times of the last zd_decode_async on the plan, in ms (HIP events on
+ * the plan's stream).  zd_plan_set_profiling mode 1: every kernel timed, the
+ * launches one after another (no K2 | K3 fork, no fused kernel); mode 2: the
+ * pipeline exactly as it runs unprofiled, with events around its dominant
+ * launch only (one entry: "zd_k_fused" in fused plans, else "zd_k_execute");
+ * 0: off.  names/ms arrays of cap entries. */
 int zd_plan_set_profiling(zd_plan* plan, int enable);
 int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, int* n);
 
@@ -256,8 +275,13 @@ int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, 
  * that sized dst from zd_plan_info_get does not plan twice).  The plan keeps
  * the device buffers for the next call (freed by zd_plan_destroy); input and
  * output move through pinned chunks (zd_plan_info io_*_ns: the phases of the
- * last call).  Not thread-safe against other zd_plan_decompress calls of the
- * process (they serialise on the pinned ring). */
+ * last call).  A frame that decodes past the capacity the plan reserved for
+ * it (its Frame_Content_Size, or 128 KiB per block) is planned again from its
+ * own start with more room, as often as needed (info.replans); the reference
+ * checks neither (decoding_context.rs:29-47, block.rs:50).  Calls on distinct
+ * plans may run on distinct threads: they share one process-wide pair of
+ * pinned chunks only while copying (the copies serialise, the decodes
+ * overlap); one plan is not used from two threads at once. */
 int zd_plan_decompress(zd_plan* plan, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 /* Convenience: host in, host out (H2D + decode + D2H on the default
  * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
@@ -328,9 +352,10 @@ int zd_comm_gather(zd_comm* comm, const uint8_t* d_local, uint64_t local_len, in
 
 /* The whole multi-GPU decode (the reference's `decode every frame of a
  * file`, sharded): every rank passes the same host input; rank `comm`'s
- * frame range is planned, copied to HBM, decoded, and gathered to rank 0
- * (zd_comm_gather).  Returns the local call's status (ZD_OK when the
- * collective completed); the input's status is res->status. */
+ * frame range is planned, copied to HBM, decoded (with zd_plan_decompress's
+ * re-plans past frames that overran their reserved capacity), and gathered
+ * to rank 0 (zd_comm_gather).  Returns the local call's status (ZD_OK when
+ * the collective completed); the input's status is res->status. */
 int zd_decode_sharded(zd_comm* comm, const uint8_t* src, size_t n, uint32_t flags, uint8_t* d_root_out,
                       uint64_t root_cap, zd_gather_result* res, void* stream);
 

@@ -24,10 +24,14 @@ for s in "$@"; do
     test)  run pytest 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     large) run pytest_large 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread tests/test_large_frames.py tests/test_resource_digests.py "tests/test_gpu_parity.py::test_hip_graph_capture_replay" ;;
     testall) run pytest_all 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    tail) run pytest_tail 1100 python -u -m pytest -x -v -p no:cacheprovider --timeout 900 --timeout-method thread -m gpu tests/test_k4f.py tests/test_large_frames.py tests/test_resource_digests.py tests/test_shard.py ;;
     t2) run pytest_t2 900 python -u -m pytest -x -v -p no:cacheprovider --timeout 600 --timeout-method thread "tests/test_gpu_parity.py::test_hip_graph_capture_replay" tests/test_shard.py tests/test_k4f.py -m gpu ;;
     benchc3s) run bench_c3s 600 python bench.py --workload c3s --steps 5 --warmup 2 --no-cpu-baseline ;;
     profc3s) run prof_c3s 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3s -o run --output-format csv -- python bench.py --workload c3s --steps 3 --warmup 1 --no-cpu-baseline ;;
     benchc3) run bench_c3 600 python bench.py --workload c3 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    nofarq) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_nofar.so run bench_nofar 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify --experiment --no-host-io ;;
+    k3q8q) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-host-io ;;
+    k3q8) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8_full 900 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline ;;

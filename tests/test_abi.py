@@ -32,7 +32,7 @@ def test_status_names():
     assert _lib.status_name(0) == "Ok"
     assert _lib.status_name(_lib.NOT_ENOUGH_BYTES) == "NotEnoughBytes"
     assert _lib.status_name(_lib.REF_PANIC) == "ReferencePanic"
-    assert _lib.lib().zd_abi_version() == 6
+    assert _lib.lib().zd_abi_version() == 7
 
 
 def test_index_resources(resources):
@@ -76,7 +76,26 @@ def test_index_block_kats():
     assert e.value.name == "NotEnoughBytes"
 
 
+def test_frames_index_headers(kat):
+    """The host index (zd_frames_index, the header pass of Frame::parse) on
+    the reference's header KATs (tests/frame.rs:155-257), no GPU."""
+    from zstd_decompressor.batch import frames_index
+    none = (1 << 64) - 1
+    for c in kat["header_parse"]:
+        if "error" in c:
+            continue
+        data = bytes([0x28, 0xB5, 0x2F, 0xFD] + c["data"] + [0x03, 0x00, 0x00, 0x00])
+        frames, _, st, _ = frames_index(data)
+        f = frames[0]
+        got = (f["window_size"], None if f["content_size"] == none else f["content_size"],
+               None if f["dict_id"] == none else f["dict_id"])
+        assert st == 0 and got == (c["window"], c["fcs"], c["dict"]), c["src"]
+
+
+@pytest.mark.gpu
 def test_frame_parse_headers(kat):
+    """Frame.parse (the crate mirror): the header pass, then the GPU pass that
+    builds the frame's tables (ZStandard::parse)."""
     from zstd_decompressor import ForwardByteParser, Frame
     for c in kat["header_parse"]:
         if "error" in c:

@@ -218,8 +218,29 @@ def _comm_world1_worker(port, q):
                                            C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
         ok2 = st2 == 0 and res2.status == 0 and res2.total_len == len(expect) and \
             bytes(out[:len(expect)].cpu().numpy().tobytes()) == expect
+        # inputs that take zd_plan_decompress's re-plan, a > 12-bit Huffman
+        # tree and a corrupt middle frame, each against the oracle (status,
+        # first failing frame, output of the frames before it)
+        bad = []
+        for name, data in _sharded_cases():
+            ost, oout = oracle.decompress_status(data, False)
+            cap = max(len(oout), 1) + 64
+            for root_cap in (cap, 16):          # in place at the root / through the comm's buffer
+                out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+                res3 = _lib.GatherResult()
+                p, n, keep = _lib.buf(data)
+                st3 = _lib.lib().zd_decode_sharded(comm._h, p, n, 0, C.c_void_p(out.data_ptr()), root_cap,
+                                                   C.byref(res3), C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+                torch.cuda.synchronize(dev)
+                if root_cap < len(oout):
+                    if not (st3 == _lib.DST_TOO_SMALL or res3.status == _lib.DST_TOO_SMALL or len(oout) == 0):
+                        bad.append((name, "small root", st3, res3.status))
+                    continue
+                got = bytes(out[:res3.total_len].cpu().numpy().tobytes())
+                if st3 != 0 or res3.status != ost or got != oout:
+                    bad.append((name, st3, res3.status, ost, res3.total_len, len(oout)))
         comm.close()
-        q.put((ok1, ok2))
+        q.put((ok1, ok2, bad))
     finally:
         dist.destroy_process_group()
 
@@ -236,7 +257,63 @@ def test_comm_gather_and_sharded_decode_world1_gpu():
     got = q.get(timeout=240)
     p.join(timeout=60)
     assert p.exitcode == 0
-    assert got == (True, True)
+    assert got == (True, True, [])
+
+
+def _lower_fcs(frame: bytes, fcs: int) -> bytes:
+    """A libzstd frame whose Frame_Content_Size field claims `fcs` bytes (the
+    reference checks no FCS, decoding_context.rs:29-47: it decodes the whole
+    frame; the GPU plan reserves fcs bytes and must re-plan)."""
+    fhd = frame[4]
+    single = (fhd >> 5) & 1
+    flen = {0: 1 if single else 0, 1: 2, 2: 4, 3: 8}[fhd >> 6]
+    at = 5 + (0 if single else 1) + {0: 0, 1: 1, 2: 2, 3: 4}[fhd & 3]
+    assert flen >= 4, "a frame with a 4- or 8-byte FCS field"
+    return frame[:at] + fcs.to_bytes(flen, "little") + frame[at + flen:]
+
+
+def _sharded_cases():
+    """Inputs for zd_decode_sharded against the oracle: an FCS-overrun frame
+    in the middle (re-planned, twice over), a > 12-bit Huffman tree frame (K2's
+    interval decode), a corrupt middle frame (the output stops before it)."""
+    import random
+    from corpus import gen
+    from test_gpu_parity import _deep_tree_frame
+    src = gen.text(1 << 20, seed=23)
+    fr = [gen.frames(src[i * 100_000:(i + 1) * 100_000], 100_000, 3) for i in range(8)]
+    r = random.Random(5)
+    deep = next(f for f in (_deep_tree_frame(r, r.randrange(20, 200), list(range(13, 0, -1))) for _ in range(200))
+                if oracle_status(f) == 0)
+    corrupt = None
+    for at in range(len(fr[3]) // 2, len(fr[3]) - 4):    # the first flip the reference rejects
+        c = bytearray(fr[3])
+        c[at] ^= 0x5A
+        if oracle_status(bytes(c)) != 0:
+            corrupt = c
+            break
+    return [
+        ("fcs overrun", b"".join(fr[:3]) + _lower_fcs(fr[3], 3000) + b"".join(fr[4:])),
+        ("fcs overrun x2", fr[0] + _lower_fcs(fr[1], 100) + _lower_fcs(fr[2], 70_000) + fr[3]),
+        ("deep tree", fr[0] + deep + fr[1] + deep + fr[2]),
+        ("corrupt middle", b"".join(fr[:3]) + bytes(corrupt) + b"".join(fr[4:])),
+    ]
+
+
+def oracle_status(data: bytes) -> int:
+    from oracle import oracle
+    return oracle.decompress_status(data, False)[0]
+
+
+def test_sharded_cases_are_what_they_claim():
+    """Host: the oracle decodes the FCS-overrun inputs fully (past their FCS),
+    and the corrupt-middle input fails at its fourth frame."""
+    from oracle import oracle
+    cases = dict(_sharded_cases())
+    for k in ("fcs overrun", "fcs overrun x2", "deep tree"):
+        st, out = oracle.decompress_status(cases[k], False)
+        assert st == 0 and len(out) > 0, k
+    st, out = oracle.decompress_status(cases["corrupt middle"], False)
+    assert st != 0 and len(out) == 300_000
 
 
 def _layout_py(meta, world):

@@ -74,6 +74,7 @@ struct zd_plan {
   uint64_t n_comps = 0, n_blocks = 0, n_frames = 0, n_tables = 0, n_huf = 0, n_seq = 0, n_k4f = 0, n_copies = 0;
   uint64_t n_jframes = 0, n_jblk = 0, n_jseg = 0;
   bool fused = false;                           // zd_k_fused plan (build_plan fuse_plan)
+  bool last_fused = false;                      // the last zd_decode_async launched zd_k_fused
   std::vector<uint64_t> frame_out, frame_cap;   // output offset and capacity per frame
   bool staged = false;
   std::unique_lock<std::mutex> stage_lock;      // the pinned staging, from build_plan to upload_plan
@@ -102,7 +103,10 @@ struct zd_plan {
     nframes = 0;
     for (const HostPart& hp : parts) { part_f0.push_back(nframes); nframes += hp.frames.size(); }
   }
-  bool profile = false;
+  bool profile = false;                  // mode 1: every kernel timed, one after another
+  bool profile_dom = false;              // mode 2: the dominant launch timed in the pipeline as it runs
+  bool dom_fused = false;                // the last mode-2 launch timed zd_k_fused (else zd_k_execute)
+  hipEvent_t dom_ev[2] = {};
   hipEvent_t ev[N_KERNELS + 1] = {};
   bool ev_made = false;
   bool launched = false;
@@ -127,11 +131,71 @@ namespace {
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-// K4F takes one workgroup per CU: rounds of 256 frames at ~0.21 ms each
-// against the streaming K4's one round (~0.75 ms) up to 4096 frames, so it
-// pays for up to three rounds (scripts/exp_thresholds.sh: 8192 frames 12.1
-// vs 7.7 ms per step)
-constexpr size_t K4F_AUTO_MIN_FRAMES = 256, K4F_AUTO_MAX_FRAMES = 3 * 256;
+// Executor routing (zd_route, a pure function of the plan's shape and the
+// device's CU count; every bound below is in units of the CU count, measured
+// on the 256-CU MI355X):
+// * K4F takes one workgroup per CU: rounds of one frame per CU at ~0.21 ms
+//   each against the streaming K4's one round (~0.75 ms) of up to 16 frames
+//   per CU, so it pays for up to three rounds (scripts/exp_thresholds.sh:
+//   8192 frames 12.1 vs 7.7 ms per step): plans of 1-3 frames per CU.
+// * zd_k_fused holds four frames per workgroup and at most one workgroup per
+//   CU beside K2 (which its K4 waves wait for): plans of 1-4 single-block
+//   frames per CU (C3: 763 frames).
+// * K1's sequence half one wave per block (zd_k_tables_seqw) while the plan
+//   fits one round of 64 tables per CU (scripts/r3_k1wmax.sh: one rank's C4
+//   share at 8 GPUs, 10,240 blocks, +1 %; full C4, 81,920 blocks, -1 %).
+// * K2 beside K3 (the fork) where K3's last round of chains (64 per CU)
+//   leaves LDS for K2: the round's fill f = (blocks mod 64 CUs) / (64 CUs),
+//   measured with K3Q on C4-shaped plans (value, no fork -> fork): 10,240
+//   blocks (f 0.63) 194 -> 221 GB/s, 20,480 (0.25) 211 -> 234, 40,960 (0.5)
+//   247 -> 253; 12,288 (0.75) 221 -> 210, 16,384 (0) 251 -> 214, 32,768 (0)
+//   266 -> 250, 81,920 (0) 273 -> 268; 763 (C3) and 8,192 (0.5) fork.  So
+//   fork when 0 < f <= 0.65 (and at least one block per CU).
+// * Without the fork, K1's two halves on the two streams (C4 273.3 -> 274.0).
+// The ZD_FUSE / ZD_K4F / ZD_FORK / ZD_K1FORK / ZD_K1W_MAX environment
+// variables are experiment overrides read once per process (route_env);
+// nothing reads them unless they are set.
+struct RouteIn {
+  uint32_t cus;
+  uint64_t nframes, n_tables, n_seq, n_huf;
+  bool single_block_frames;      // every frame a zstd frame of one compressed block, no host-found error
+  bool context;                  // a DecodingContext plan (existing output or prebuilt tables)
+  uint32_t flags;                // ZD_F_*
+};
+struct Route {
+  bool fused = false, k4f = false, k1_seq_waves = false, fork = false, k1_fork = false;
+};
+constexpr uint32_t K4F_MIN_PER_CU = 1, K4F_MAX_PER_CU = 3;
+constexpr uint32_t FUSE_MIN_PER_CU = 1, FUSE_MAX_PER_CU = 4;
+constexpr uint32_t K1W_MAX_PER_CU = 64;
+constexpr uint32_t K3_CHAINS_PER_CU = 64;
+constexpr double FORK_MAX_FILL = 0.65;
+Route route_plan(const RouteIn& in) {
+  Route r;
+  const uint64_t cus = std::max<uint32_t>(in.cus, 1);
+  r.fused = !(in.flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) && !in.context &&
+            in.single_block_frames && in.nframes >= FUSE_MIN_PER_CU * cus && in.nframes <= FUSE_MAX_PER_CU * cus;
+  r.k4f = !r.fused && in.nframes >= K4F_MIN_PER_CU * cus && in.nframes <= K4F_MAX_PER_CU * cus;
+  r.k1_seq_waves = in.n_tables <= K1W_MAX_PER_CU * cus && !(in.flags & ZD_F_K1_LANES);
+  const uint64_t slots = K3_CHAINS_PER_CU * cus, rem = in.n_seq % slots;
+  r.fork = in.n_seq >= cus && rem != 0 && (double)rem <= FORK_MAX_FILL * (double)slots;
+  r.k1_fork = !r.fork && in.n_huf && in.n_seq;
+  return r;
+}
+// The environment overrides (experiments only), read once
+struct RouteEnv {
+  int fuse = -1, k4f = -1, fork = -1, k1fork = -1;
+  int64_t k1w_max = -1;
+  RouteEnv() {
+    auto get = [](const char* n) { const char* e = getenv(n); return e ? atoi(e) : -1; };
+    fuse = get("ZD_FUSE"); k4f = get("ZD_K4F"); fork = get("ZD_FORK"); k1fork = get("ZD_K1FORK");
+    if (const char* e = getenv("ZD_K1W_MAX")) k1w_max = atoll(e);
+  }
+};
+const RouteEnv& route_env() {
+  static const RouteEnv e;
+  return e;
+}
 // K4J (block-parallel execute, pointer jumping) takes the frames of at least
 // K4J_MIN_BLOCKS compressed blocks: the streaming K4 runs a frame's blocks one
 // after another on one wave, which a frame of many blocks cannot hide behind
@@ -471,39 +535,38 @@ HostStage& host_stage() {
 constexpr uint64_t STAGE_MIN_BYTES = 1u << 20;     // smaller plans fill host vectors
 
 // K3's chains in flight on the current device: 64 per CU (LDS-bound)
+// (the CU count of each device, cached under a lock: plans are made and
+// launched from several threads)
 size_t k3_slots() {
-  static int dev_cached = -1;
-  static size_t slots = 64 * 256;
+  static std::mutex m;
+  static std::vector<int> cus_of;
   int dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess && dev != dev_cached) {
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) { (void)hipGetLastError(); return 64 * 256; }
+  std::lock_guard<std::mutex> g(m);
+  if ((size_t)dev >= cus_of.size()) cus_of.resize((size_t)dev + 1, 0);
+  if (!cus_of[(size_t)dev]) {
     int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-      slots = 64 * (size_t)cus;
-    dev_cached = dev;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+    cus_of[(size_t)dev] = cus;
   }
-  return slots;
+  return 64 * (size_t)cus_of[(size_t)dev];
 }
 
-// zd_k_fused: K3 and K4 fused per group of four frames, for plans of few
-// single-block frames (the few-frames regime, C3: 763 frames).  Up to one
-// workgroup per CU, so K2's workgroups (which the fused K4 waves wait for)
-// always find room beside them.  ZD_FUSE=0/1 forces it off/on where allowed.
-constexpr size_t FUSE_MIN_FRAMES = 256;
-// zd_k_tables_seqw up to this many tables (scripts/r3_k1wmax.sh, bench value
-// lanes -> waves: one rank's C4 share at 8 GPUs, 10,240 blocks, 237 -> 241 and
-// 234 -> 237 GB/s; full C4, 81,920 blocks, 274 -> 270)
-constexpr uint64_t K1W_MAX_BLOCKS = 16384;
-bool fuse_plan(const zd_plan* P, uint64_t out_len0) {
-  static const char* env = getenv("ZD_FUSE");
-  if (env && atoi(env) == 0) return false;
-  if ((P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) || out_len0 || P->has_prebuilt)
-    return false;
-  const size_t cus = k3_slots() / 64;
-  if (P->nframes < (env ? 1 : FUSE_MIN_FRAMES) || P->nframes > 4 * cus) return false;
+// The plan's routing inputs (host frames, device CU count)
+RouteIn route_in(const zd_plan* P, uint64_t out_len0) {
+  RouteIn in{};
+  in.cus = (uint32_t)(k3_slots() / 64);
+  in.nframes = P->nframes;
+  in.context = out_len0 != 0 || P->has_prebuilt;
+  in.flags = P->flags;
+  in.single_block_frames = true;
   for (const HostPart& hp : P->parts)
     for (const HostFrame& hf : hp.frames)
-      if (hf.d.kind != ZD_FRAME_ZSTD || hf.key != KEY_NONE || hf.nb != 1) return false;
-  return true;
+      if (hf.d.kind != ZD_FRAME_ZSTD || hf.key != KEY_NONE || hf.nb != 1) in.single_block_frames = false;
+  return in;
 }
 
 // Builds device-side descriptors from the host frames: one counting pass and
@@ -523,10 +586,19 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   for (const HostPart& hp : P->parts)
     if (!hp.frames.empty()) { X.cap0_frame = hp.frames.data(); break; }
   X.flags = P->flags;
-  static const char* k4f_env = getenv("ZD_K4F");
-  X.k4f_on = k4f_env ? atoi(k4f_env) == 1 : P->nframes >= K4F_AUTO_MIN_FRAMES && P->nframes <= K4F_AUTO_MAX_FRAMES;
-  X.fused = fuse_plan(P, out_len0);
-  if (X.fused) X.k4f_on = false;
+  {
+    const RouteIn in = route_in(P, out_len0);
+    const Route r = route_plan(in);
+    const RouteEnv& E = route_env();
+    X.fused = r.fused;
+    // ZD_FUSE=1 forces the fused kernel on any plan of single-block frames
+    // (its K2 then runs before it, not beside it, zd_decode_async); 0 off
+    if (E.fuse == 0) X.fused = false;
+    if (E.fuse == 1) X.fused = !(P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) && !in.context &&
+                               in.single_block_frames && P->nframes >= 1;
+    X.k4f_on = E.k4f >= 0 ? E.k4f == 1 : r.k4f;
+    if (X.fused) X.k4f_on = false;
+  }
   static const char* k4j_env = getenv("ZD_K4J");
   X.k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0 : (k4j_env ? atoi(k4j_env) : -1);
   X.k4j_min = P->nframes <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
@@ -700,22 +772,6 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   I.index_status = P->index_status;
   I.executors = (P->fused ? ZD_EXEC_FUSED : 0u) | (P->n_k4f ? ZD_EXEC_K4F : 0u) | (P->n_jframes ? ZD_EXEC_K4J : 0u);
   return 0;
-}
-
-// K2 | K3 fork: it pays where K3's last round of chains leaves LDS for K2
-// beside it.  K3 holds 64 chains per CU (4 workgroups of 16); with the round's
-// fill f = (blocks mod 64 CUs) / (64 CUs), measured with K3Q on C4-shaped
-// plans (value, no fork -> fork): 10,240 blocks (f 0.63) 194 -> 221 GB/s,
-// 20,480 (0.25) 211 -> 234, 40,960 (0.5) 247 -> 253; 12,288 (0.75) 221 ->
-// 210, 16,384 (0) 251 -> 214, 32,768 (0) 266 -> 250, 81,920 (0) 273 -> 268;
-// 763 (C3) and 8,192 (0.5) fork.  So: fork when 0 < f <= 0.65.
-constexpr size_t FORK_MIN_SEQ_BLOCKS = 256;
-constexpr double FORK_MAX_FILL = 0.65;
-bool fork_auto(size_t n_seq) {
-  const size_t slots = k3_slots();
-  if (n_seq < FORK_MIN_SEQ_BLOCKS) return false;
-  const size_t rem = n_seq % slots;
-  return rem != 0 && (double)rem <= FORK_MAX_FILL * (double)slots;
 }
 
 // Device workspaces of destroyed plans, kept for the next plans of this
@@ -1040,21 +1096,21 @@ DevWalkBufs& dev_walk_bufs() {
 template <typename T>
 bool grow_dev(T*& p, size_t& cap, size_t need) {
   if (need <= cap) return true;
+  const size_t n = need;
   if (p) (void)hipFree(p);
   p = nullptr;
   cap = 0;
-  const size_t n = std::max(need, cap * 2);
-  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) return false;
+  if (hipMalloc(&p, n * sizeof(T)) != hipSuccess) { (void)hipGetLastError(); return false; }
   cap = n;
   return true;
 }
 template <typename T>
 bool grow_pinned(T*& p, size_t& cap, size_t need) {
   if (need <= cap) return true;
+  const size_t n = need;
   if (p) (void)hipHostFree(p);
   p = nullptr;
   cap = 0;
-  const size_t n = std::max(need, cap * 2);
   if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) return false;
   cap = n;
   return true;
@@ -1102,9 +1158,13 @@ void par_memcpy(uint8_t* d, const uint8_t* s, size_t n) {
     memcpy(d + a, s + a, b - a);
   });
 }
+// The ring is held only while its slots are in use: the H2D copy returns
+// after its last DMA (the stream synchronised), the D2H copy after its last
+// host copy, so decodes on other plans or devices run beside it.
 int io_h2d(uint8_t* d, const uint8_t* h, size_t n, hipStream_t s, IoRing& R, hipEvent_t ev[2]) {
   if (!n) return 0;
-  if (!R.ok()) { HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s)); return 0; }
+  std::lock_guard<std::mutex> lk(R.m);
+  if (!R.ok()) { HIPCHK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s)); HIPCHK(hipStreamSynchronize(s)); return 0; }
   for (size_t o = 0, k = 0; o < n; o += IO_CHUNK, k++) {
     const size_t c = std::min<size_t>(IO_CHUNK, n - o);
     if (k >= 2) HIPCHK(hipEventSynchronize(ev[k & 1]));   // chunk k - 2's DMA out of this slot
@@ -1112,10 +1172,12 @@ int io_h2d(uint8_t* d, const uint8_t* h, size_t n, hipStream_t s, IoRing& R, hip
     HIPCHK(hipMemcpyAsync(d + o, R.p[k & 1], c, hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(ev[k & 1], s));
   }
+  HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
 int io_d2h(uint8_t* h, const uint8_t* d, size_t n, hipStream_t s, IoRing& R, hipEvent_t ev[2]) {
   if (!n) return 0;
+  std::lock_guard<std::mutex> lk(R.m);
   if (!R.ok()) { HIPCHK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s)); HIPCHK(hipStreamSynchronize(s)); return 0; }
   const size_t nk = (n + IO_CHUNK - 1) / IO_CHUNK;
   auto chunk = [&](size_t k) { return std::min<size_t>(IO_CHUNK, n - k * IO_CHUNK); };
@@ -1326,6 +1388,19 @@ extern "C" {
 
 int zd_abi_version(void) { return ZD_ABI_VERSION; }
 
+int zd_route(uint32_t cus, uint64_t nframes, uint64_t n_tables, uint64_t n_seq_blocks, uint64_t n_huf_blocks,
+             int single_block_frames, uint32_t flags, uint32_t* route) {
+  if (!route || !cus) return ZD_E_INVALID_ARG;
+  RouteIn in{};
+  in.cus = cus; in.nframes = nframes; in.n_tables = n_tables; in.n_seq = n_seq_blocks; in.n_huf = n_huf_blocks;
+  in.single_block_frames = single_block_frames != 0;
+  in.flags = flags;
+  const Route r = route_plan(in);
+  *route = (r.fused ? ZD_ROUTE_FUSED : 0u) | (r.k4f ? ZD_ROUTE_K4F : 0u) | (r.k1_seq_waves ? ZD_ROUTE_K1_SEQ_WAVES : 0u) |
+           (r.fork ? ZD_ROUTE_FORK : 0u) | (r.k1_fork ? ZD_ROUTE_K1_FORK : 0u);
+  return ZD_OK;
+}
+
 void zd_trim_cache(void) { ws_trim(-1); }
 
 const char* zd_status_name(int s) {
@@ -1514,23 +1589,39 @@ void zd_plan_destroy(zd_plan* P) {
   if (P->d_meta) (void)hipFree(P->d_meta);
   if (P->io_src) (void)hipFree(P->io_src);
   if (P->io_dst) (void)hipFree(P->io_dst);
-  if (P->ev_made) for (auto& e : P->ev) (void)hipEventDestroy(e);
+  if (P->ev_made) {
+    for (auto& e : P->ev) (void)hipEventDestroy(e);
+    for (auto& e : P->dom_ev) (void)hipEventDestroy(e);
+  }
   aux_give(P);
   delete P;
 }
 
 int zd_plan_set_profiling(zd_plan* P, int enable) {
-  if (!P) return ZD_E_INVALID_ARG;
+  if (!P || enable < 0 || enable > 2) return ZD_E_INVALID_ARG;
   if (enable && !P->ev_made) {
     for (auto& e : P->ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : P->dom_ev) HIPCHK(hipEventCreate(&e));
     P->ev_made = true;
   }
-  P->profile = enable != 0;
+  P->profile = enable == 1;
+  P->profile_dom = enable == 2;
   return ZD_OK;
 }
 
 int zd_plan_kernel_times(zd_plan* P, const char** names, float* ms, int cap, int* n) {
-  if (!P || !P->profile || !P->launched) return ZD_E_INVALID_ARG;
+  if (!P || !P->launched || !(P->profile || P->profile_dom)) return ZD_E_INVALID_ARG;
+  if (P->profile_dom) {
+    HIPCHK(hipEventSynchronize(P->dom_ev[1]));
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, P->dom_ev[0], P->dom_ev[1]));
+    if (cap > 0) {
+      if (names) names[0] = P->dom_fused ? "zd_k_fused" : "zd_k_execute";
+      if (ms) ms[0] = t;
+    }
+    if (n) *n = cap > 0 ? 1 : 0;
+    return ZD_OK;
+  }
   HIPCHK(hipEventSynchronize(P->ev[N_KERNELS]));
   int k = 0;
   for (; k < N_KERNELS && k < cap; k++) {
@@ -1587,29 +1678,33 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // plan flag ZD_F_SEQ_ONE_LANE keeps the one-lane chain (same records)
   a.k3_quad = !(P->flags & ZD_F_SEQ_ONE_LANE);
   a.events = P->profile ? P->ev : nullptr;
-  // K2 beside K3 on a second stream: slower where K3's rounds fill the LDS
-  // (full C4: K3 is LDS-bound and K2 takes its CUs), faster where K3's last
-  // round leaves room (fork_auto); ZD_FORK=1 / 0 (read once) forces it on / off
-  static const char* fork_env = getenv("ZD_FORK");
-  const bool fork = fork_env ? atoi(fork_env) == 1 : fork_auto(P->n_seq);
+  // routing (route_plan): K2 beside K3 on a second stream, K1's halves on
+  // the two streams, K1's sequence half one wave per block
+  RouteIn in{};
+  in.cus = (uint32_t)(k3_slots() / 64);
+  in.nframes = P->n_frames; in.n_tables = P->n_tables; in.n_seq = P->n_seq; in.n_huf = P->n_huf;
+  in.flags = P->flags;
+  const Route r = route_plan(in);
+  const RouteEnv& E = route_env();
+  // (a forced fused plan past FUSE_MAX_PER_CU frames per CU: K2 before it, its
+  // workgroups could not find room beside the fused ones)
+  const bool big_fused = P->fused && P->n_frames > FUSE_MAX_PER_CU * (uint64_t)in.cus;
+  const bool fork = E.fork >= 0 ? E.fork == 1 && !big_fused : r.fork && !big_fused;
   if (fork) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
-  // no fork: K1's Huffman half on the second stream beside its sequence
-  // half, joined before K2 (ZD_K1FORK=0 / 1, read once)
-  static const char* k1f_env = getenv("ZD_K1FORK");
-  if (!fork && !P->profile && P->n_huf && P->n_seq && (k1f_env ? atoi(k1f_env) == 1 : true)) {
+  if (!fork && !P->profile && (E.k1fork >= 0 ? E.k1fork == 1 && P->n_huf && P->n_seq : r.k1_fork)) {
     a.aux = P->aux; a.fork = P->fork; a.join = P->join;
     a.k1_fork = true;
   }
-  // K1's sequence half one wave per block in plans of few tables (C3 with
-  // ZD_F_NO_FUSE / c3s, 763 blocks: 0.25 -> 0.06 ms); the plan flag
-  // ZD_F_K1_LANES keeps the lanes, ZD_K1W_MAX (read once) moves the bound
-  static const char* k1w_env = getenv("ZD_K1W_MAX");   // (read once) the block-count bound
-  const uint64_t k1w_max = k1w_env ? (uint64_t)atoll(k1w_env) : K1W_MAX_BLOCKS;
-  a.k1_seq_waves = P->n_tables <= k1w_max && !(P->flags & ZD_F_K1_LANES);
-  if (P->fused && !P->profile) {
+  a.k1_seq_waves = E.k1w_max >= 0 ? P->n_tables <= (uint64_t)E.k1w_max && !(P->flags & ZD_F_K1_LANES) : r.k1_seq_waves;
+  P->last_fused = P->fused && !P->profile;
+  if (P->last_fused) {
     a.fused = true;
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.redo, 0, std::max<uint64_t>(P->n_frames, 1), s));
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.k2done, 0, 4, s));
+  }
+  if (P->profile_dom) {
+    a.dom_events = P->dom_ev;
+    P->dom_fused = a.fused;
   }
   HIPCHK(launch_pipeline(a));
   P->launched = true;
@@ -1685,6 +1780,14 @@ int zd_plan_results(zd_plan* P, uint8_t* d_dst, void* stream, int32_t* frame_sta
     HIPCHK(hipStreamSynchronize(s));
   }
   if (first < 0 && P->index_status) { first = (int)nf; overall = P->index_status; }
+  // frames zd_k_fused handed to its redo pass (a fast-chain reject, or a wait
+  // past its bound: a slowdown, never a different output)
+  P->info.fused_redo_frames = 0;
+  if (P->last_fused && nf) {
+    std::vector<uint8_t> redo(nf);
+    HIPCHK(hipMemcpy(redo.data(), P->d_ws + P->W.redo, nf, hipMemcpyDeviceToHost));
+    for (uint8_t r : redo) P->info.fused_redo_frames += r != 0;
+  }
   P->res_off = to;
   P->res_len = len;
   if (total_len) *total_len = total;
@@ -1716,41 +1819,35 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
   return ZD_OK;
 }
 
-// One decode of plan P, host in / host out: the frames before the first
-// failure land in dst (up to cap bytes), *total = their length.
-static int plan_decompress_once(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
-                                uint64_t* total) {
-  const uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
-  // device buffers owned by the plan (kept for the next call), the input and
-  // output through the pinned ring (chunked, the host copies on the worker
-  // pool overlapping the DMA), everything on one stream
-  if (!grow_dev(P->io_src, P->io_src_cap, n + ZD_SRC_PADDING) || !grow_dev(P->io_dst, P->io_dst_cap, ob))
-    return ZD_E_HIP;
-  const hipStream_t s = nullptr;
-  IoRing& R = io_ring();
-  std::lock_guard<std::mutex> lk(R.m);
-  IoEvents ev;
-  if (!ev.ok) return ZD_E_HIP;
-  const auto t0 = std::chrono::steady_clock::now();
-  if (int r = io_h2d(P->io_src, src, n, s, R, ev.e)) return r;
+}  // extern "C"
+
+namespace {
+
+// Makes o hold `need` bytes, keeping its first `keep` (a new allocation in
+// the caller's *o.own when o is short; o.p itself is freed only when it is
+// that allocation).
+int devout_reserve(DevOut& o, uint64_t need, uint64_t keep, hipStream_t s) {
+  if (need <= o.cap) return 0;
+  const uint64_t want = std::max<uint64_t>(need, o.cap + o.cap / 2);
+  uint8_t* q = nullptr;
+  if (hipMalloc(&q, want) != hipSuccess) {
+    (void)hipGetLastError();
+    ws_trim(-1);
+    HIPCHK(hipMalloc(&q, want));
+  }
+  if (keep) HIPCHK(hipMemcpyAsync(q, o.p, keep, hipMemcpyDeviceToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
-  const auto t1 = std::chrono::steady_clock::now();
-  int r = zd_decode_async(P, P->io_src, P->io_dst, ob, s);
-  int32_t first = -1;
-  *total = 0;
-  if (!r) r = zd_plan_results(P, P->io_dst, s, nullptr, nullptr, total, &first);
-  if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG || r == ZD_E_DST_TOO_SMALL) return r;
-  const auto t2 = std::chrono::steady_clock::now();
-  const size_t copy = (size_t)std::min<uint64_t>(*total, cap);
-  if (copy && dst)
-    if (int e = io_d2h(dst, P->io_dst, copy, s, R, ev.e)) return e;
-  const auto t3 = std::chrono::steady_clock::now();
-  auto ns = [](auto a, auto b) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count(); };
-  P->info.io_h2d_ns = ns(t0, t1);
-  P->info.io_decode_ns = ns(t1, t2);
-  P->info.io_d2h_ns = ns(t2, t3);
-  return r;
+  if (*o.own) (void)hipFree(*o.own);        // the old kept allocation (o.p or unused)
+  *o.own = q;
+  *o.own_cap = want;
+  o.p = q;
+  o.cap = want;
+  return 0;
 }
+
+bool call_failed(int st) { return st == ZD_E_HIP || st == ZD_E_INVALID_ARG || st == ZD_E_DST_TOO_SMALL; }
+
+}  // namespace
 
 // Re-plans past a frame that reached a limit the host can lift: a frame that
 // decodes past the capacity its plan reserved (its Frame_Content_Size, or
@@ -1758,18 +1855,26 @@ static int plan_decompress_once(zd_plan* P, const uint8_t* src, size_t n, uint8_
 // 29-47, block.rs:50) is planned again from its own start with four times the
 // capacity (K4_MAX_FRAME_OUT at most); a K4J frame whose pointer jumping did
 // not converge is planned again on the streaming executor.  Each re-plan
-// covers the input from that frame on; its output follows the frames before.
+// covers the input from that frame on (the same resident input, from that
+// frame's offset); its output follows the frames before in `out`.
 constexpr int LIMIT_RETRIES = 12;
 
-int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
-  if (!P || (!src && n) || n != P->info.src_bytes) return ZD_E_INVALID_ARG;
-  uint64_t total = 0;
-  int st = plan_decompress_once(P, src, n, dst, cap, &total);
-  if (st == ZD_E_HIP || st == ZD_E_INVALID_ARG || st == ZD_E_DST_TOO_SMALL) return st;
-  uint64_t produced = total;
-  P->info.replans = 0;
+int zd::decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t* d_src, DevOut& out, void* stream,
+                        uint64_t* total_out, int64_t* first_out, uint64_t* replans) {
+  const hipStream_t s = (hipStream_t)stream;
+  *total_out = 0;
+  *first_out = -1;
+  const uint64_t ob = std::max<uint64_t>(P->info.out_bytes, 16);
+  if (int r = devout_reserve(out, ob, 0, s)) return r;
+  int st = zd_decode_async(P, d_src, out.p, out.cap, s);
+  if (st) return st;
+  uint64_t produced = 0;
+  int32_t first = -1;
+  st = zd_plan_results(P, out.p, s, nullptr, nullptr, &produced, &first);
+  if (call_failed(st)) return st;
   zd_plan* cur = P;
   size_t base = 0;                                 // cur's input starts at src + base
+  int64_t fbase = 0;                               // and its frame 0 is P's frame fbase
   for (int k = 0; k < LIMIT_RETRIES && st == ZD_E_OUT_OF_DOMAIN && cur->limit_frame >= 0; k++) {
     const size_t f = (size_t)cur->limit_frame;
     const uint64_t old_cap = cur->frame_cap[f];
@@ -1786,21 +1891,60 @@ int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, s
     zd_plan* Q = nullptr;
     const int r = plan_create(src + at, nullptr, n - at, flags, nullptr, &Q, cap0);
     if (r) { st = r; break; }
-    P->info.replans++;
+    if (replans) (*replans)++;
+    const uint64_t qob = std::max<uint64_t>(Q->info.out_bytes, 16);
     uint64_t t2 = 0;
-    const uint64_t room = cap > produced ? cap - produced : 0;
-    st = plan_decompress_once(Q, src + at, n - at, room ? dst + produced : nullptr, room, &t2);
+    int32_t qfirst = -1;
+    st = devout_reserve(out, produced + qob, produced, s);
+    if (!st) st = zd_decode_async(Q, d_src + at, out.p + produced, qob, s);
+    if (!st) st = zd_plan_results(Q, out.p + produced, s, nullptr, nullptr, &t2, &qfirst);
     if (cur != P) zd_plan_destroy(cur);
     cur = Q;
     base = at;
-    if (st == ZD_E_HIP || st == ZD_E_INVALID_ARG || st == ZD_E_DST_TOO_SMALL) break;
+    fbase += (int64_t)f;
+    first = qfirst;
+    if (call_failed(st)) break;
     produced += t2;
   }
   if (cur != P) {
     P->info.error_key = cur->info.error_key;
     zd_plan_destroy(cur);
   }
-  if (st == ZD_E_HIP || st == ZD_E_INVALID_ARG) return st;
+  if (call_failed(st)) return st;
+  *total_out = produced;
+  *first_out = first >= 0 ? fbase + first : -1;
+  return st;
+}
+
+extern "C" {
+
+int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+  if (!P || (!src && n) || n != P->info.src_bytes) return ZD_E_INVALID_ARG;
+  // device buffers owned by the plan (kept for the next call), the input and
+  // output through the pinned ring (chunked, the host copies on the worker
+  // pool overlapping the DMA), everything on one stream
+  if (!grow_dev(P->io_src, P->io_src_cap, n + ZD_SRC_PADDING)) return ZD_E_HIP;
+  const hipStream_t s = nullptr;
+  IoEvents ev;
+  if (!ev.ok) return ZD_E_HIP;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (int r = io_h2d(P->io_src, src, n, s, io_ring(), ev.e)) return r;
+  const auto t1 = std::chrono::steady_clock::now();
+  DevOut o{P->io_dst, P->io_dst_cap, &P->io_dst, &P->io_dst_cap};
+  uint64_t produced = 0;
+  int64_t first = -1;
+  P->info.replans = 0;
+  const int st = decode_resident(P, src, n, P->io_src, o, s, &produced, &first, &P->info.replans);
+  if (call_failed(st)) return st;
+  const auto t2 = std::chrono::steady_clock::now();
+  const size_t copy = (size_t)std::min<uint64_t>(produced, cap);
+  if (copy && dst)
+    if (int e = io_d2h(dst, o.p, copy, s, io_ring(), ev.e)) return e;
+  const auto t3 = std::chrono::steady_clock::now();
+  auto ns = [](auto a, auto b) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count(); };
+  P->info.io_h2d_ns = ns(t0, t1);
+  P->info.io_decode_ns = ns(t1, t2);
+  P->info.io_d2h_ns = ns(t2, t3);
   if (out_len) *out_len = (size_t)produced;
   if (!st && produced > cap) return ZD_E_DST_TOO_SMALL;
   return st;

@@ -1716,6 +1716,13 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
       outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
       if constexpr (PUB) {
+        // The line published here ends with pair slot - 14, seven pairs back;
+        // each pair since issued K3_PAIR_VMEM vector-memory ops (two window
+        // loads of N / 4 dwordx4 (+ one dwordx2) each, one store), so
+        // vmcnt(32) has drained that store only when 7 pairs issue more than
+        // 32 ops (N = 6 or 8: 35; N = 4 would leave it in flight)
+        constexpr int K3_PAIR_VMEM = 2 * (N / 4 + (N % 4 == 2 ? 1 : 0)) + 1;
+        static_assert(7 * K3_PAIR_VMEM > 32, "seq_chainq PUB: vmcnt(32) would not cover the published line's stores");
         if (((slot + 2) & 15) == 0 && slot + 2 >= 32) {
           asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
           if (role == 0) *prog = (slot + 2 - 16) >> 4;
@@ -1739,7 +1746,11 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   return (mx >= K3F_BAD || ymin < 0 || pl < 0 || E > pl) ? 1 : 0;
 }
 
-constexpr int K3Q_CHAINS = 16;          // blocks per workgroup (one wave, four lanes each)
+#ifndef ZD_K3Q_CHAINS
+#define ZD_K3Q_CHAINS 16
+#endif
+constexpr int K3Q_CHAINS = ZD_K3Q_CHAINS;   // blocks per workgroup (one wave, four lanes each)
+static_assert(K3Q_CHAINS == 8 || K3Q_CHAINS == 16, "K3Q: 8 or 16 chains per wave");
 __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict__ src,
                                                        const CompBlock* __restrict__ comp, CompState* cstate,
                                                        FrameState* fstate, const uint32_t* __restrict__ list,
@@ -1749,7 +1760,7 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
   const int lane = threadIdx.x;
   const int role = lane & 3, q = lane >> 2;
   const uint32_t li = blockIdx.x * K3Q_CHAINS + q;
-  bool act = li < n_list;
+  bool act = q < K3Q_CHAINS && li < n_list;
   const uint32_t ci = act ? list[li] : 0;
   CompBlock C;
   if (act) C = comp[ci];
@@ -1869,7 +1880,15 @@ __device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
 // Match sources in HBM are read through the caches: the frame's own recent
 // output, re-read by later matches (plain loads: the nontemporal form took
 // 28.3 ms against 23.4 in round 1)
+#ifdef ZD_EXP_NOFAR
+// timing-only experiment build (wrong output): every match source that
+// would come from HBM comes from the window in LDS instead
+__device__ inline u32x4 ldg16_src(const uint8_t* p) {
+  return *(const l_u32x4a1*)(const l_u8*)(uintptr_t)((uintptr_t)p & 2047);
+}
+#else
 __device__ inline u32x4 ldg16_src(const uint8_t* p) { return *(g_cu32x4a1*)p; }
+#endif
 // streams read once (records, literals): plain loads (nontemporal loads of
 // the records, windows and literal stage measured slower: 1 GiB K4 2.06 ->
 // 2.11 ms)
@@ -2142,8 +2161,11 @@ __device__ inline bool k4f_wait_k2(const K4Fuse& z) {
     if (!ok) __builtin_amdgcn_s_sleep(ZD_FZ_SLEEP);
   }
   if (ok && z.k2need) {
+    // bounded near K2's own time (fused plans hold <= 4 frames per CU: K2
+    // takes well under 1 ms there); a wait past ~30 ms sends the frame to the
+    // redo pass, which zd_plan_info.fused_redo_frames reports
     ok = false;
-    for (uint32_t it = 0; it < (1u << 22) && !ok; it++) {
+    for (uint32_t it = 0; it < (1u << 15) && !ok; it++) {
       ok = __hip_atomic_load(z.k2done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= z.k2need;
       if (!ok) __builtin_amdgcn_s_sleep(32);
     }
@@ -4153,9 +4175,11 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     // two launches whose workgroups exit at once)
     uint8_t* redo = ws + W.redo;
     const uint32_t k2need = fork ? (a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS : 0;
+    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[0], s)) != hipSuccess) return e;
     hipLaunchKernelGGL(zd_k_fused, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * FZ_WAVES), 0, s,
                        a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
                        fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
+    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[1], s)) != hipSuccess) return e;
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, redo);
@@ -4165,7 +4189,9 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
+    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[0], s)) != hipSuccess) return e;
     k4(0, a.n_frames, s, nullptr);
+    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[1], s)) != hipSuccess) return e;
     k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s);
   }
   if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;

@@ -26,6 +26,10 @@ struct LaunchArgs {
   bool fused = false;                      // K3 + K4 as zd_k_fused, then the redo pass
   bool k1_seq_waves = false;               // K1's sequence half one wave per block (zd_k_tables_seqw)
   bool k1_fork = false;                    // no K2 | K3 fork: K1's halves on the two streams (aux, fork, join)
+  // optional: two events recorded on `stream` around the pipeline's dominant
+  // launch as it runs (zd_k_fused in fused plans, else zd_k_execute), with
+  // the fork and fusion kept (zd_plan_set_profiling mode 2)
+  hipEvent_t* dom_events = nullptr;
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.

@@ -250,7 +250,7 @@ int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, 
   uint64_t sb = 0, se = 0, fb = 0, fe = 0;
   if (int r = zd_shard_range(src, n, c->rank, c->world, &sb, &se, &fb, &fe)) return r;
   int32_t status = ZD_OK;
-  int32_t first = -1;
+  int64_t first = -1;
   uint64_t len = 0;
   uint8_t* d_out = nullptr;
   zd_plan* P = nullptr;
@@ -263,17 +263,19 @@ int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, 
       zd_plan_info info;
       zd_plan_info_get(P, &info);
       const uint64_t ob = std::max<uint64_t>(info.out_bytes, 16);
-      // rank 0's range comes first in the output: it decodes in place
-      d_out = (c->rank == 0 && root_cap >= ob) ? d_root_out : nullptr;
       if (!grow(c->d_src, c->src_cap, se - sb + ZD_SRC_PADDING)) { err = ZD_E_HIP; break; }
-      if (!d_out) {
-        if (!grow(c->d_out, c->out_cap, ob)) { err = ZD_E_HIP; break; }
-        d_out = c->d_out;
-      }
       if (hipMemcpyAsync(c->d_src, src + sb, se - sb, hipMemcpyHostToDevice, s) != hipSuccess) { err = ZD_E_HIP; break; }
-      if ((err = zd_decode_async(P, c->d_src, d_out, ob, s))) break;
-      const int r = zd_plan_results(P, d_out, s, nullptr, nullptr, &len, &first);
-      if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG) { err = r; break; }
+      // rank 0's range comes first in the output: it decodes in place (until
+      // a re-plan outgrows the root buffer: then into the communicator's own,
+      // and the gather copies it over)
+      zd::DevOut o = (c->rank == 0 && root_cap >= ob) ? zd::DevOut{d_root_out, root_cap, &c->d_out, &c->out_cap}
+                                                     : zd::DevOut{c->d_out, c->out_cap, &c->d_out, &c->out_cap};
+      // the same decode as zd_plan_decompress, re-plans past frames that
+      // overran their reserved capacity included
+      uint64_t replans = 0;
+      const int r = zd::decode_resident(P, src + sb, se - sb, c->d_src, o, s, &len, &first, &replans);
+      if (r == ZD_E_HIP || r == ZD_E_INVALID_ARG || r == ZD_E_DST_TOO_SMALL) { err = r; break; }
+      d_out = o.p;
       status = r;
     } while (0);
     if (err) { status = err; len = 0; first = 0; }

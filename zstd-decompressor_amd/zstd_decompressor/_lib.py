@@ -45,7 +45,8 @@ class PlanInfo(C.Structure):
                 ("index_status", C.c_int32), ("executors", C.c_uint32), ("host_ns", C.c_uint64),
                 ("device_ns", C.c_uint64), ("walk_serial_bytes", C.c_uint64),
                 ("io_h2d_ns", C.c_uint64), ("io_decode_ns", C.c_uint64), ("io_d2h_ns", C.c_uint64),
-                ("error_key", C.c_uint64), ("replans", C.c_uint64)]
+                ("error_key", C.c_uint64), ("replans", C.c_uint64),
+                ("fused_redo_frames", C.c_uint64)]
 
 
 class GatherResult(C.Structure):
@@ -59,6 +60,8 @@ COMM_ID_BYTES = 128
 _u8p, _sz, _szp, _vp = C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_size_t), C.c_void_p
 SIGNATURES = {
     "zd_status_name": (C.c_char_p, [C.c_int]),
+    "zd_route": (C.c_int, [C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, C.c_uint32,
+                           C.POINTER(C.c_uint32)]),
     "zd_abi_version": (C.c_int, []),
     "zd_trim_cache": (None, []),
     "zd_frames_index": (C.c_int, [_vp, _sz, C.POINTER(FrameDesc), _sz, _szp, C.POINTER(BlockDesc), _sz, _szp, _szp]),

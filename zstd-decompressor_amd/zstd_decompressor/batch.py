@@ -54,6 +54,35 @@ def decompress(data: bytes, print_skippable: bool = False) -> bytes:
     return out
 
 
+KEY_NONE = (1 << 64) - 1
+PH_PARSE = 0
+
+
+def decode_keyed(data: bytes, flags: int = 0):
+    """(status, output of the frames before the first failure, error key):
+    one plan and zd_plan_decompress; the key's phase (key >> 62: 0 parse, 1
+    decode, 3 a limit) tells a table-description error, which the reference
+    raises in Frame::parse, from an execution error it raises in decode."""
+    L = _lib.lib()
+    plan = Plan(data, bool(flags & _lib.F_SKIPPABLE), flags & ~_lib.F_SKIPPABLE)
+    try:
+        cap = max(plan.info.out_bytes, 1)
+        p, n, keep = _lib.buf(data)
+        for _ in range(2):
+            out = (C.c_uint8 * cap)()
+            ol = C.c_size_t()
+            st = L.zd_plan_decompress(plan._h, p, n, out, cap, C.byref(ol))
+            if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
+                _lib.check(st, "zd_plan_decompress")
+            if ol.value <= cap:
+                break
+            cap = ol.value
+        key = plan.refresh_info().error_key
+        return st, bytes(out[: min(ol.value, cap)]), key
+    finally:
+        plan.close()
+
+
 def decompress_status(data: bytes, print_skippable: bool = False, flags: int = 0):
     """(status, output of the frames before the first failure).  flags: extra
     zd_plan flags (_lib.F_BLOCK_PARALLEL / F_FRAME_SERIAL pick the executor)."""
@@ -89,8 +118,15 @@ class Plan:
         _lib.check(L.zd_plan_info_get(h, C.byref(self.info)), "zd_plan_info_get")
         return self
 
-    def set_profiling(self, on: bool = True):
+    def set_profiling(self, on=True):
+        """zd_plan_set_profiling: True / 1 every kernel timed one after another,
+        2 the pipeline as it runs with events around its dominant launch, 0 off."""
         _lib.check(_lib.lib().zd_plan_set_profiling(self._h, int(on)))
+
+    def refresh_info(self):
+        """zd_plan_info again (the fields of the last decode / results)."""
+        _lib.check(_lib.lib().zd_plan_info_get(self._h, C.byref(self.info)), "zd_plan_info_get")
+        return self.info
 
     def decode_async(self, d_src: int, d_dst: int, dst_cap: int, stream: int = 0):
         """Launch the pipeline; pointers/stream are integers (e.g. tensor.data_ptr(),

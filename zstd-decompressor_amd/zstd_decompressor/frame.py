@@ -1,11 +1,15 @@
 """Frame layer (frame.rs): Frame, ZStandard, Skippable, Header, FrameIterator.
 
 Frame.parse runs the host index (zd_frames_index: FrameIterator/Frame::parse/
-Header::parse/Block::parse structure, frame.rs:61-230); Frame.decode runs the
-HIP pipeline (zd_decompress) — ZStandard::decode (frame.rs:232-260).
-Differences from the Rust API: entropy-table errors that the reference raises
-inside Frame::parse (Huffman/FSE descriptions) are raised by decode(), which
-is where the GPU parses those tables.
+Header::parse/Block::parse structure, frame.rs:61-230) and then the HIP
+pipeline on the frame: ZStandard::parse builds every block's Huffman and FSE
+tables and fails there (frame.rs:198-230, literals.rs:88-133,
+sequences.rs:91-143), and the GPU builds those tables in its first kernel, so
+an error in a table description (error key phase 0, parse) is raised by
+Frame.parse as in the reference, whatever block it is in; the frame's output
+or its execution error (phase 1) is kept for decode() (ZStandard::decode,
+frame.rs:232-260).  Host-only callers that want the index without a GPU
+pass use zd_frames_index (batch.frames_index).
 """
 from __future__ import annotations
 
@@ -41,9 +45,10 @@ class Skippable:                  # frame.rs:55-58
 
 
 class ZStandard:                  # frame.rs:189-272
-    def __init__(self, raw: bytes, d: FrameDesc, blocks):
+    def __init__(self, raw: bytes, d: FrameDesc, blocks, decoded=None):
         self._raw, self._d, self._blocks = raw, d, blocks
         self._header = Header(d)
+        self._decoded = decoded       # (status, output) of the GPU pass Frame.parse ran
 
     def header(self) -> Header:
         return self._header
@@ -55,8 +60,12 @@ class ZStandard:                  # frame.rs:189-272
         return self._blocks
 
     def decode(self) -> bytes:
-        from .batch import decompress
-        return decompress(self._raw)
+        if self._decoded is None:
+            from .batch import decompress
+            return decompress(self._raw)
+        st, out = self._decoded
+        _lib.check(st, "ZStandard::decode")
+        return out
 
 
 class Frame:
@@ -88,8 +97,12 @@ class Frame:
         if d.kind == 1:
             return Frame(Skippable(d.magic, raw[8:]))
         from .block import Block
+        from .batch import decode_keyed, KEY_NONE, PH_PARSE
         blocks = [Block._from_desc(raw, ba[i], d.src_offset) for i in range(nb.value)]
-        return Frame(ZStandard(raw, d, blocks))
+        fst, out, key = decode_keyed(raw)
+        if fst != 0 and key != KEY_NONE and (key >> 62) == PH_PARSE:
+            raise ZdError(fst, "Frame::parse")        # a Huffman / FSE table description (ZStandard::parse)
+        return Frame(ZStandard(raw, d, blocks, (fst, out)))
 
     def decode(self) -> bytes:
         return self.inner.decode()
