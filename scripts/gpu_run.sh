@@ -7,6 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export ZD_CORPUS_CACHE=${ZD_CORPUS_CACHE:-/tmp/zd_corpus}   # corpora shared by the steps of one call
 fatal() { case "$1" in 124|134|137|139|132|135|136) return 0;; *) return 1;; esac; }
 run() {  # name seconds cmd...
   local name=$1 secs=$2; shift 2
@@ -32,6 +33,7 @@ for s in "$@"; do
     nofarq) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_nofar.so run bench_nofar 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify --experiment --no-host-io ;;
     k3q8q) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-host-io ;;
     k3q8) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8_full 900 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
+    benchnc) run bench_nc 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline ;;
