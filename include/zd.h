@@ -194,6 +194,9 @@ typedef struct zd_plan_info {
   uint64_t fused_redo_frames; /* the last zd_plan_results of a zd_k_fused launch: frames its redo
                               pass decoded (a fast-chain reject, or a wait for K2 / the chain
                               past its bound); 0 normally, never a different output */
+  uint64_t device_descriptors; /* 1: zd_plan_create_device built the descriptors on the GPU from its
+                              own index (only the frames' output offsets and capacities came
+                              back); 0: the index came back and the host built them */
 } zd_plan_info;
 
 /* The executor routing zd_plan_create / zd_decode_async choose for a plan of

@@ -34,6 +34,7 @@ for s in "$@"; do
     k3q8q) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-host-io ;;
     k3q8) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8_full 900 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     benchnc) run bench_nc 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
+    walk) run pytest_walk 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu tests/test_gpu_walk.py ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench_quick 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline ;;

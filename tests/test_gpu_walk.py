@@ -90,3 +90,42 @@ def test_device_walk_false_frame_costs_one_range():
     assert _decode(dp, d_src, dev) == _decode(hp, d_src, dev)
     hp.close()
     dp.close()
+
+
+def test_device_descriptors(tmp_path):
+    """SURVEY §8f1's rest: when the device walk's chains meet (no stitch) and no
+    frame goes to K4J, zd_plan_create_device builds the descriptors on the GPU
+    (zd_k_plan_count / zd_k_plan_fill: the host planner's own per-frame pass,
+    zd_plan.h) and reads back only the totals and the frames' output offsets
+    and capacities (info.device_descriptors).  The plan equals the host
+    planner's descriptor for descriptor, with and without -p, and decodes the
+    same; a C4-shaped plan of 2,048 single-block frames and the host-walk
+    inputs with skippable frames or a failing frame take that path."""
+    import torch
+    import test_host_walk
+    from zstd_decompressor.batch import Plan
+    dev = torch.device("cuda", 0)
+    inputs = dict(test_host_walk._inputs())
+    c4 = gen.frames(gen.text(64 << 20, seed=94), 128 << 10, 3)          # 512 frames
+    cases = [("c4 x4", c4 * 4, True), ("intact", inputs["intact"], True), ("skippable", inputs["skippable"], True)]
+    for i in range(6):
+        cases.append((f"corrupt {i}", inputs[f"corrupt {i}"], False))
+    took = 0
+    for name, data, must in cases:
+        for skip in (False, True):
+            d_src = torch.zeros(len(data) + 64, dtype=torch.uint8, device=dev)
+            d_src[: len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+            torch.cuda.synchronize(dev)
+            hp, hd = _dump(str(tmp_path / "h.bin"), lambda: Plan(data, skip))
+            dp, dd = _dump(str(tmp_path / "d.bin"),
+                           lambda: Plan.from_device(d_src.data_ptr(), len(data), skip,
+                                                    stream=torch.cuda.current_stream(dev).cuda_stream))
+            assert hp.info.device_descriptors == 0
+            assert not must or dp.info.device_descriptors == 1, f"{name}: the device build was not taken"
+            took += dp.info.device_descriptors
+            assert dd == hd, f"{name} (-p {skip}): device descriptors differ from the host planner's"
+            if not skip:
+                assert _decode(dp, d_src, dev) == _decode(hp, d_src, dev), name
+            hp.close()
+            dp.close()
+    assert took >= 6

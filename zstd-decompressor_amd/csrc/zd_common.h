@@ -450,6 +450,7 @@ struct Workspace {
   uint64_t huge;                                        // K1: u32 count + the blocks whose trees have > 256 symbols
   uint64_t jst;                                         // K4J per-byte state words
   uint64_t redo, k2done;                                // zd_k_fused: frames for the redo pass, K2's finished workgroups
+  uint64_t hframes;                                     // device-built plans: the walk's frame index (zd_walk.h HostFrame)
   uint64_t total;
 };
 

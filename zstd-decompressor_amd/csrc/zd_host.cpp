@@ -25,6 +25,7 @@
 #include "zd_common.h"
 #include "zd_internal.h"
 #include "zd_launch.h"
+#include "zd_plan.h"
 #include "zd_walk.h"
 
 using namespace zd;
@@ -93,7 +94,20 @@ struct zd_plan {
   int64_t limit_frame = -1;
   uint32_t limit_stage = 0;
   size_t index_stop = 0;                 // frame index that failed to index (== nframes - 1) or nframes
+  // a plan whose descriptors the GPU built (zd_plan_create_device): its
+  // frame index stays in the workspace (W.hframes) until a caller needs it
+  bool dev_built = false;
+  mutable std::vector<HostFrame> dev_frames;
   const HostFrame& frame(size_t f) const {
+    if (dev_built) {
+      if (dev_frames.size() != nframes) {
+        dev_frames.resize(nframes);
+        if (nframes && hipMemcpy(dev_frames.data(), d_ws + W.hframes, nframes * sizeof(HostFrame),
+                                 hipMemcpyDeviceToHost) != hipSuccess)
+          (void)hipGetLastError();
+      }
+      return dev_frames[f];
+    }
     const size_t k = (size_t)(std::upper_bound(part_f0.begin(), part_f0.end(), f) - part_f0.begin()) - 1;
     return parts[k].frames[f - part_f0[k]];
   }
@@ -196,251 +210,8 @@ const RouteEnv& route_env() {
   static const RouteEnv e;
   return e;
 }
-// K4J (block-parallel execute, pointer jumping) takes the frames of at least
-// K4J_MIN_BLOCKS compressed blocks: the streaming K4 runs a frame's blocks one
-// after another on one wave, which a frame of many blocks cannot hide behind
-// other frames unless the plan holds thousands of them
-// (K4J_MAX_FRAMES).  ZD_K4J=1 / 0 forces it on (every frame with a
-// compressed block) / off.
-constexpr uint32_t K4J_MIN_BLOCKS = 16;
-constexpr size_t K4J_MAX_FRAMES = 1024;
-// A plan of few frames leaves the GPU nearly idle with one wave per frame on
-// the streaming K4 (the reference's moby-dick sample: one frame of 10 blocks,
-// 159k sequences on one wave): there K4J takes every frame of 2 or more
-// compressed blocks.
-constexpr size_t K4J_FEW_FRAMES = 64;
-constexpr uint32_t K4J_MIN_BLOCKS_FEW = 2;
 constexpr size_t PAR_INDEX_MIN_BYTES = 4u << 20;    // the host walk in parallel from 4 MiB of input (>= 512 frames)
 constexpr size_t FRAMES_INDEX_SERIAL_MAX = 4096;     // zd_frames_index asked for at most this many frames: walk only them
-
-// Running indices of build_plan: every array it fills grows frame by frame,
-// so a frame's entries start at the counts of the frames before it.
-struct PlanCounts {
-  uint64_t frames = 0, blocks = 0, comps = 0, luts = 0, fses = 0, lits = 0, nrec = 0, nseq = 0, out = 0;
-  uint64_t tables = 0, huf = 0, seq = 0, k4f = 0, copies = 0;
-  uint64_t jframes = 0, jblk = 0, jseg = 0;
-  bool exact = true;
-  void add(const PlanCounts& o) {
-    frames += o.frames; blocks += o.blocks; comps += o.comps; luts += o.luts; fses += o.fses; lits += o.lits;
-    nrec += o.nrec; nseq += o.nseq; out += o.out; tables += o.tables; huf += o.huf; seq += o.seq; k4f += o.k4f;
-    copies += o.copies; jframes += o.jframes; jblk += o.jblk; jseg += o.jseg; exact = exact && o.exact;
-  }
-};
-
-// Plan-wide inputs of the per-frame pass.  `prev_*` seed the Treeless/Repeat
-// resolution (context API), -1 when absent.
-struct PlanCtx {
-  int32_t prev_huf;
-  int32_t prev_tab[3];
-  uint64_t out_len0, fixed_cap, cap0;
-  const HostFrame* cap0_frame;   // the plan's first frame (cap0 applies to it)
-  uint64_t rep0[3];
-  uint32_t flags;
-  bool k4f_on, k4j_auto;
-  bool fused;              // zd_k_fused plan: no K4F, 128-byte aligned literal and record slots
-  int k4j_mode;
-  uint32_t k4j_min;        // compressed blocks a frame needs for K4J (automatic mode)
-};
-
-// Where the filling pass writes: the plan's host vectors (small plans, the
-// context API) or the pinned upload staging at the workspace offsets.
-struct Sink {
-  CompBlock* comps;
-  BlockRec* blocks;
-  FrameDesc* fdesc;
-  FrameState* fstate0;
-  uint32_t *list_tables, *list_huf, *list_seq, *list_k4f;
-  CopyDesc* copies;
-  JFrame* jframes;
-  JBlkDesc* jblkd;
-  JSegDesc* jsegd;
-  uint64_t *frame_out, *frame_cap;
-};
-
-// One frame's descriptors at the running indices c (build_plan).  FILL: the
-// entries are written to S; otherwise c only advances (the counting pass).
-// Frames for K4J are listed in *jfr (their descriptors come after, in order).
-template <bool FILL>
-void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks, PlanCounts& c, const Sink& S,
-                std::vector<uint32_t>* jfr) {
-  const uint32_t fi = (uint32_t)c.frames;
-  FrameDesc fd{};
-  FrameState fs{};
-  fs.key = hf.key;
-  fs.rep[0] = X.rep0[0]; fs.rep[1] = X.rep0[1]; fs.rep[2] = X.rep0[2];
-  fd.first_block = (uint32_t)c.blocks;
-  fd.out_len0 = X.out_len0;
-  int32_t huf_prev = X.prev_huf;
-  int32_t tab_prev[3] = {X.prev_tab[0], X.prev_tab[1], X.prev_tab[2]};
-  uint64_t bound = 0;
-  bool seqs_in_frame = false;
-  const bool frame_failed_host = hf.key != KEY_NONE;
-  uint64_t jseg = 0;
-  // a re-plan of a frame that overran (zd_plan_decompress): by identity, the
-  // counting pass numbers each part's frames from 0
-  const bool replanned = X.cap0 && &hf == X.cap0_frame && hf.d.kind == ZD_FRAME_ZSTD;
-  for (uint32_t bi = 0; bi < hf.nb; bi++) {
-    const HostBlock& hb = hblocks[hf.b0 + bi];
-    BlockRec br{};
-    br.src = hb.src; br.size = hb.size; br.type = hb.type; br.last = hb.last; br.rle = hb.rle; br.comp = -1;
-    if (hb.type == 2) {
-      CompBlock cb = hb.cb;
-      cb.frame = fi;
-      cb.block_in_frame = bi;
-      cb.prebuilt = 0;
-      cb.huf_src = -1;
-      cb.tab_src[0] = cb.tab_src[1] = cb.tab_src[2] = -1;
-      const uint32_t ci = (uint32_t)c.comps;
-      const bool failing = cb.host_stage != PS_ALL;
-      // literals: Treeless resolution (literals.rs:59-66)
-      if (!failing && (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS)) {
-        if (cb.lit_type == LIT_COMPRESSED) { cb.huf_src = (int32_t)ci; huf_prev = (int32_t)ci; }
-        else cb.huf_src = huf_prev;
-        if (cb.huf_src < 0)
-          fs.key = std::min(fs.key, make_key(PH_DECODE, bi, DS_LITERALS, 0, ZD_E_HUFFMAN_DECODER_MISSING));
-      }
-      if (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) cb.lut_slot = (uint32_t)c.luts++;
-      // sequences: Repeat resolution (sequences.rs:147-187, 232-234)
-      if (!failing) {
-        if (cb.nseq == 0) {
-          int code = ZD_E_EMPTY_INPUT_DATA;
-          for (int k = 0; k < 3; k++) if (tab_prev[k] < 0) { code = ZD_E_NO_PREVIOUS_DECODER; break; }
-          fs.key = std::min(fs.key, make_key(PH_DECODE, bi, DS_SEQUENCES, 0, code));
-        } else {
-          cb.fse_slot = (uint32_t)c.fses++;
-          bool miss = false;
-          for (int k = 0; k < 3; k++) {
-            if (cb.modes[k] == M_REPEAT) {
-              if (tab_prev[k] < 0) { miss = true; break; }
-              cb.tab_src[k] = tab_prev[k];
-            } else {
-              cb.tab_src[k] = (int32_t)ci;
-            }
-          }
-          if (miss) fs.key = std::min(fs.key, make_key(PH_DECODE, bi, DS_SEQUENCES, 0, ZD_E_NO_PREVIOUS_DECODER));
-          else for (int k = 0; k < 3; k++) tab_prev[k] = cb.tab_src[k];
-        }
-      } else if (cb.nseq) {
-        cb.fse_slot = (uint32_t)c.fses++;
-      }
-      // workspace
-      if (cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) {
-        cb.lit_extra = 0;
-        if (replanned) {             // a symbol is at least one bit: <= 8 literals per stream byte
-          uint64_t most = 0;
-          for (int k = 0; k < cb.nstreams; k++) most += 8ull * cb.stream_size[k];
-          if (most > cb.lit_regen) cb.lit_extra = (uint32_t)(most - cb.lit_regen);
-        }
-        cb.lit_out = c.lits;
-        c.lits += align_up((uint64_t)cb.lit_regen + 24 + cb.lit_extra, X.fused ? 128 : 16);   // + K2's 8-byte slack
-      }
-      if (X.fused) c.nrec = align_up(c.nrec, 16);   // a block's records start a 128-byte line
-      cb.seq_out = c.nrec;
-      c.nseq += cb.nseq;
-      c.nrec += rec_slots(cb.nseq);              // record pairs, a spare pair past the block's last
-      seqs_in_frame |= cb.nseq > 0;
-      br.comp = (int32_t)ci;
-      jseg += cb.nseq > J_SEG ? (cb.nseq + J_SEG - 1) / J_SEG : 1;
-      const bool needs_tables = (cb.lit_type == LIT_COMPRESSED && cb.host_stage > PS_HUF_DESC) ||
-                                (cb.nseq > 0 && cb.host_stage > PS_SEQ_TABLES);
-      if (needs_tables) { if (FILL) S.list_tables[c.tables] = ci; c.tables++; }
-      if (!frame_failed_host) {
-        if ((cb.lit_type == LIT_COMPRESSED || cb.lit_type == LIT_TREELESS) && cb.nstreams && cb.huf_src >= 0) {
-          if (FILL) S.list_huf[c.huf] = ci;
-          c.huf++;
-        }
-        if (cb.nseq > 0 && cb.tab_src[0] >= 0 && cb.tab_src[1] >= 0 && cb.tab_src[2] >= 0) {
-          if (FILL) S.list_seq[c.seq] = ci;
-          c.seq++;
-        }
-      }
-      if (FILL) S.comps[ci] = cb;
-      c.comps++;
-      bound += MAX_BLOCK_OUT;
-    } else {
-      bound += hb.size;
-      jseg += 1;
-    }
-    if (FILL) S.blocks[c.blocks] = br;
-    c.blocks++;
-  }
-  fd.nblocks = hf.nb;
-  uint64_t cap;
-  if (hf.d.kind == ZD_FRAME_SKIPPABLE) {
-    // a truncated skippable frame fails to index and keeps no payload block
-    cap = ((X.flags & ZD_F_SKIPPABLE) && hf.nb) ? hblocks[hf.b0].size : 0;
-    if (!(X.flags & ZD_F_SKIPPABLE)) fd.nblocks = 0;
-  } else if (hf.d.content_size != UINT64_MAX && hf.d.content_size <= bound) {
-    cap = hf.d.content_size;
-  } else {
-    cap = bound;
-    c.exact = false;
-  }
-  if (frame_failed_host) fd.nblocks = 0;
-  if (X.fixed_cap) cap = X.fixed_cap;
-  if (replanned) {
-    cap = X.cap0;
-    c.exact = false;
-  }
-  fd.out = c.out;
-  fd.out_cap = cap;
-  // K4J: frames of many compressed blocks (u32 positions)
-  const bool to_j = X.out_len0 == 0 && !frame_failed_host && fd.nblocks && hf.ncomp && hf.d.kind == ZD_FRAME_ZSTD &&
-                    cap <= K4J_MAX_FRAME_OUT &&
-                    (X.k4j_mode >= 0 ? X.k4j_mode == 1 : (X.k4j_auto && hf.ncomp >= X.k4j_min));
-  // the streaming K4 keeps int32 frame positions: larger frames with
-  // sequences that K4J does not take are outside the GPU path's domain
-  if (!to_j && cap > K4_MAX_FRAME_OUT && seqs_in_frame)
-    fs.key = std::min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
-  if (to_j) {
-    fd.lds = 2;
-    c.jframes++;
-    c.jblk += fd.nblocks;
-    c.jseg += jseg;
-    if (FILL) jfr->push_back(fi);
-  } else {
-    // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
-    // executes the frames that fit it in plans of 256-768 frames, where the
-    // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
-    // it is slower on C4.  ZD_K4F=1 / 0 forces it on / off.
-    fd.lds = (X.k4f_on && X.out_len0 == 0 && cap <= K4F_CAP) ? 1u : 0u;
-  }
-  if (fd.lds == 1) { if (FILL) S.list_k4f[c.k4f] = fi; c.k4f++; }
-  // Leading raw / RLE blocks (skippable payloads too) have output offsets
-  // known here: K0 copies them in parallel pieces, the streaming K4 starts
-  // after them (a frame of raw/RLE blocks only never reaches K4's loop).
-  if (!fd.lds && fd.nblocks && cap < 0x7FF00000ull) {
-    uint64_t pre = 0;
-    uint32_t k = 0;
-    for (; k < fd.nblocks; k++) {
-      const HostBlock& hb = hblocks[hf.b0 + k];
-      if (hb.type != 0 && hb.type != 1 && hb.type != 4) break;
-      if (X.out_len0 + pre + hb.size > cap) break;
-      for (uint64_t x = 0; x < hb.size; x += COPY_PIECE) {
-        if (FILL) {
-          CopyDesc cd{};
-          cd.src = hb.src + (hb.type == 1 ? 0 : x);
-          cd.dst = c.out + X.out_len0 + pre + x;
-          cd.size = (uint32_t)std::min<uint64_t>(COPY_PIECE, hb.size - x);
-          cd.fill = hb.type == 1 ? (0x100u | hb.rle) : 0u;
-          S.copies[c.copies] = cd;
-        }
-        c.copies++;
-      }
-      pre += hb.size;
-    }
-    fd.skip = k;
-    fd.skip_bytes = pre;
-  }
-  if (FILL) {
-    S.frame_out[fi] = c.out;
-    S.frame_cap[fi] = cap;
-    S.fdesc[fi] = fd;
-    S.fstate0[fi] = fs;
-  }
-  c.out += cap;
-  c.frames++;
-}
 
 // A process-wide pool of host worker threads (created on first use, kept:
 // spawning 15 threads per planner pass cost ~0.3 ms each time).
@@ -555,27 +326,27 @@ size_t k3_slots() {
   return 64 * (size_t)cus_of[(size_t)dev];
 }
 
-// The plan's routing inputs (host frames, device CU count)
-RouteIn route_in(const zd_plan* P, uint64_t out_len0) {
-  RouteIn in{};
-  in.cus = (uint32_t)(k3_slots() / 64);
-  in.nframes = P->nframes;
-  in.context = out_len0 != 0 || P->has_prebuilt;
-  in.flags = P->flags;
-  in.single_block_frames = true;
-  for (const HostPart& hp : P->parts)
-    for (const HostFrame& hf : hp.frames)
-      if (hf.d.kind != ZD_FRAME_ZSTD || hf.key != KEY_NONE || hf.nb != 1) in.single_block_frames = false;
-  return in;
+// K4J's mode from the plan flags (ZD_K4J=1 / 0, read once, forces it on / off)
+int k4j_mode_of(uint32_t flags) {
+  static const char* k4j_env = getenv("ZD_K4J");
+  return (flags & ZD_F_BLOCK_PARALLEL) ? 1 : (flags & ZD_F_FRAME_SERIAL) ? 0 : (k4j_env ? atoi(k4j_env) : -1);
 }
 
-// Builds device-side descriptors from the host frames: one counting pass and
-// one filling pass over the parts in parallel (each part's entries start at
-// the counts of the parts before it), then the K4J descriptors in frame order.
-// `staged`: a large plan may fill the pinned staging (zd_plan_create); the
-// context API keeps host vectors it edits afterwards.
-int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
-               const uint64_t rep0[3], uint64_t fixed_cap, bool staged = false) {
+// Every frame of the host walk a zstd frame of one compressed block, with no
+// walk-found error (the fused kernel's plans)
+bool host_single_block_frames(const zd_plan* P) {
+  for (const HostPart& hp : P->parts)
+    for (const HostFrame& hf : hp.frames)
+      if (hf.d.kind != ZD_FRAME_ZSTD || hf.key != KEY_NONE || hf.nb != 1) return false;
+  return true;
+}
+
+// The per-frame pass's plan-wide inputs (routing included): `single` =
+// every frame a single-block zstd frame, `j_candidates` = frames K4J would
+// take in automatic mode (frames without a walk-found error and with at
+// least k4j_min compressed blocks; counted only when the mode is automatic).
+PlanCtx plan_ctx(const zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
+                 const uint64_t rep0[3], uint64_t fixed_cap, bool single, uint64_t j_candidates) {
   PlanCtx X{};
   X.prev_huf = prev_huf;
   for (int k = 0; k < 3; k++) { X.prev_tab[k] = prev_tab[k]; X.rep0[k] = rep0[k]; }
@@ -586,48 +357,31 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   for (const HostPart& hp : P->parts)
     if (!hp.frames.empty()) { X.cap0_frame = hp.frames.data(); break; }
   X.flags = P->flags;
-  {
-    const RouteIn in = route_in(P, out_len0);
-    const Route r = route_plan(in);
-    const RouteEnv& E = route_env();
-    X.fused = r.fused;
-    // ZD_FUSE=1 forces the fused kernel on any plan of single-block frames
-    // (its K2 then runs before it, not beside it, zd_decode_async); 0 off
-    if (E.fuse == 0) X.fused = false;
-    if (E.fuse == 1) X.fused = !(P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) && !in.context &&
-                               in.single_block_frames && P->nframes >= 1;
-    X.k4f_on = E.k4f >= 0 ? E.k4f == 1 : r.k4f;
-    if (X.fused) X.k4f_on = false;
-  }
-  static const char* k4j_env = getenv("ZD_K4J");
-  X.k4j_mode = (P->flags & ZD_F_BLOCK_PARALLEL) ? 1 : (P->flags & ZD_F_FRAME_SERIAL) ? 0 : (k4j_env ? atoi(k4j_env) : -1);
+  RouteIn in{};
+  in.cus = (uint32_t)(k3_slots() / 64);
+  in.nframes = P->nframes;
+  in.context = out_len0 != 0 || P->has_prebuilt;
+  in.flags = P->flags;
+  in.single_block_frames = single;
+  const Route r = route_plan(in);
+  const RouteEnv& E = route_env();
+  X.fused = r.fused;
+  // ZD_FUSE=1 forces the fused kernel on any plan of single-block frames
+  // (its K2 then runs before it, not beside it, zd_decode_async); 0 off
+  if (E.fuse == 0) X.fused = false;
+  if (E.fuse == 1) X.fused = !(P->flags & (ZD_F_NO_FUSE | ZD_F_SEQ_ONE_LANE | ZD_F_BLOCK_PARALLEL)) && !in.context &&
+                             single && P->nframes >= 1;
+  X.k4f_on = E.k4f >= 0 ? E.k4f == 1 : r.k4f;
+  if (X.fused) X.k4f_on = false;
+  X.k4j_mode = k4j_mode_of(P->flags);
   X.k4j_min = P->nframes <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
-  size_t j_candidates = 0;
-  if (X.k4j_mode < 0 && out_len0 == 0)
-    for (const HostPart& hp : P->parts)
-      for (const HostFrame& hf : hp.frames) j_candidates += hf.key == KEY_NONE && hf.ncomp >= X.k4j_min;
-  X.k4j_auto = j_candidates > 0 && j_candidates <= K4J_MAX_FRAMES;
+  X.k4j_auto = X.k4j_mode < 0 && out_len0 == 0 && j_candidates > 0 && j_candidates <= K4J_MAX_FRAMES;
+  return X;
+}
 
-  const size_t np = P->parts.size();
-  std::vector<PlanCounts> cnt(np + 1);
-  const Sink none{};
-  run_parts(np, [&](size_t k) {
-    const HostPart& hp = P->parts[k];
-    PlanCounts c;
-    for (const HostFrame& hf : hp.frames) plan_frame<false>(X, hf, hp.blocks.data(), c, none, nullptr);
-    if (X.fused) {          // parts start aligned, so the filling pass pads exactly as this count did
-      c.lits = align_up(c.lits, 128);
-      c.nrec = align_up(c.nrec, 16);
-    }
-    cnt[k + 1] = c;
-  });
-  for (size_t k = 1; k <= np; k++) { PlanCounts t = cnt[k - 1]; t.add(cnt[k]); cnt[k] = t; }
-  const PlanCounts T = cnt[np];
-
-  // workspace carve-up: the arrays the host fills first (one upload), then
-  // the device-only ones
-  Workspace& W = P->W;
-  uint64_t o = 0;
+// The descriptor arrays at the head of the workspace (a host-filled plan
+// uploads them at once)
+void carve_head(Workspace& W, const PlanCounts& T, uint64_t& o) {
   auto carve = [&](uint64_t bytes) { uint64_t r = o; o = align_up(o + bytes, 256); return r; };
   W.comp = carve(sizeof(CompBlock) * std::max<uint64_t>(T.comps, 1));
   W.blocks = carve(sizeof(BlockRec) * std::max<uint64_t>(T.blocks, 1));
@@ -641,12 +395,98 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   W.jframes = carve(sizeof(JFrame) * std::max<uint64_t>(T.jframes, 1));
   W.jblkd = carve(sizeof(JBlkDesc) * std::max<uint64_t>(T.jblk, 1));
   W.jsegd = carve(sizeof(JSegDesc) * std::max<uint64_t>(T.jseg, 1));
-  P->desc_bytes = o;
-
+}
+// The device-only arrays after them (K4J's sizes from its descriptors)
+void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint64_t j_base, uint64_t j_pieces,
+                uint64_t j_maxseq) {
+  auto carve = [&](uint64_t bytes) { uint64_t r = o; o = align_up(o + bytes, 256); return r; };
+  W.comp_state = carve(sizeof(CompState) * std::max<uint64_t>(T.comps, 1));
+  W.huge = carve(4 * (std::max<uint64_t>(T.tables, 1) + 1));
+  W.frame_state = carve(sizeof(FrameState) * std::max<uint64_t>(T.frames, 1));
+  W.lits = carve(T.lits + 64);
+  W.seqs = carve(8 * T.nrec + 64);
+  W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint64_t>(T.luts, 1));
+  W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint64_t>(T.fses, 1));
+  // K4J: pointer jumping resolves every match byte within ceil(log2(matches
+  // + 1)) rounds (each pointer chain ends at a literal after at most one hop
+  // per earlier match; each round halves the hops left)
+  P->j_bytes = T.jframes ? j_base + 16 : 0;
+  P->j_pieces = j_pieces;
+  P->j_rounds = 0;
+  if (T.jframes) {
+    uint32_t r = 1;
+    while (r < (uint32_t)J_MAX_ROUNDS - 1 && (1ull << r) <= j_maxseq + 1) r++;
+    P->j_rounds = r + 1;
+  }
+  W.jblk = carve(sizeof(JBlk) * std::max<uint64_t>(T.jblk, 1));
+  W.jseg = carve(sizeof(JSeg) * std::max<uint64_t>(T.jseg, 1));
+  W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
+  W.jdone = carve(std::max<uint64_t>(j_pieces, 1));
+  W.jst = carve(4 * P->j_bytes + 64);
+  W.redo = carve(std::max<uint64_t>(T.frames, 1));
+  W.k2done = carve(4);
+}
+// The plan's array counts from the totals
+void plan_totals(zd_plan* P, const PlanCounts& T, bool fused) {
   P->n_comps = T.comps; P->n_blocks = T.blocks; P->n_frames = T.frames;
   P->n_tables = T.tables; P->n_huf = T.huf; P->n_seq = T.seq; P->n_k4f = T.k4f; P->n_copies = T.copies;
   P->n_jframes = T.jframes; P->n_jblk = T.jblk; P->n_jseg = T.jseg;
-  P->fused = X.fused && T.jframes == 0 && T.k4f == 0;
+  P->fused = fused && T.jframes == 0 && T.k4f == 0;
+}
+void plan_info(zd_plan* P, const PlanCounts& T) {
+  zd_plan_info& I = P->info;
+  I.nframes = T.frames;
+  I.nblocks = T.blocks;
+  I.ncompressed = T.comps;
+  I.out_bytes = T.out;
+  I.out_exact = T.exact();
+  I.workspace_bytes = P->W.total;
+  I.nsequences = T.nseq;
+  I.nliterals = T.lits;
+  I.index_status = P->index_status;
+  I.executors = (P->fused ? ZD_EXEC_FUSED : 0u) | (P->n_k4f ? ZD_EXEC_K4F : 0u) | (P->n_jframes ? ZD_EXEC_K4J : 0u);
+}
+
+// Builds device-side descriptors from the host frames: one counting pass and
+// one filling pass over the parts in parallel (each part's entries start at
+// the counts of the parts before it), then the K4J descriptors in frame order.
+// `staged`: a large plan may fill the pinned staging (zd_plan_create); the
+// context API keeps host vectors it edits afterwards.
+int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t out_len0,
+               const uint64_t rep0[3], uint64_t fixed_cap, bool staged = false) {
+  uint64_t j_candidates = 0;
+  if (k4j_mode_of(P->flags) < 0 && out_len0 == 0) {
+    const uint32_t k4j_min = P->nframes <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
+    for (const HostPart& hp : P->parts)
+      for (const HostFrame& hf : hp.frames) j_candidates += hf.key == KEY_NONE && hf.ncomp >= k4j_min;
+  }
+  const PlanCtx X = plan_ctx(P, prev_huf, prev_tab, out_len0, rep0, fixed_cap, host_single_block_frames(P),
+                             j_candidates);
+
+  const size_t np = P->parts.size();
+  std::vector<PlanCounts> cnt(np + 1);
+  const Sink none{};
+  run_parts(np, [&](size_t k) {
+    const HostPart& hp = P->parts[k];
+    PlanCounts c;
+    for (const HostFrame& hf : hp.frames) plan_frame<false, std::vector<uint32_t>>(X, hf, hp.blocks.data(), c, none, nullptr);
+    if (X.fused) {          // parts start aligned, so the filling pass pads exactly as this count did
+      c.lits = align_up(c.lits, 128);
+      c.nrec = align_up(c.nrec, 16);
+    }
+    cnt[k + 1] = c;
+  });
+  for (size_t k = 1; k <= np; k++) { PlanCounts t = cnt[k - 1]; t.add(cnt[k]); cnt[k] = t; }
+  const PlanCounts T = cnt[np];
+
+  // workspace carve-up: the arrays the host fills first (one upload), then
+  // the device-only ones
+  Workspace& W = P->W;
+  W = Workspace{};
+  uint64_t o = 0;
+  carve_head(W, T, o);
+  P->desc_bytes = o;
+  plan_totals(P, T, X.fused);
   P->frame_out.resize(T.frames);
   P->frame_cap.resize(T.frames);
   Sink S{};
@@ -697,7 +537,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   run_parts(np, [&](size_t k) {
     const HostPart& hp = P->parts[k];
     PlanCounts c = cnt[k];
-    for (const HostFrame& hf : hp.frames) plan_frame<true>(X, hf, hp.blocks.data(), c, S, &jfr[k]);
+    for (const HostFrame& hf : hp.frames) plan_frame<true, std::vector<uint32_t>>(X, hf, hp.blocks.data(), c, S, &jfr[k]);
   });
 
   // K4J descriptors, frames in order
@@ -733,44 +573,10 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
     }
   }
 
-  W.comp_state = carve(sizeof(CompState) * std::max<uint64_t>(T.comps, 1));
-  W.huge = carve(4 * (std::max<uint64_t>(T.tables, 1) + 1));
-  W.frame_state = carve(sizeof(FrameState) * std::max<uint64_t>(T.frames, 1));
-  W.lits = carve(T.lits + 64);
-  W.seqs = carve(8 * T.nrec + 64);
-  W.luts = carve((uint64_t)LUT_ENTRIES * 2 * std::max<uint64_t>(T.luts, 1));
-  W.fses = carve((uint64_t)FSE_SLOT * 2 * std::max<uint64_t>(T.fses, 1));
-  // K4J: pointer jumping resolves every match byte within ceil(log2(matches
-  // + 1)) rounds (each pointer chain ends at a literal after at most one hop
-  // per earlier match; each round halves the hops left)
-  P->j_bytes = T.jframes ? j_base + 16 : 0;
-  P->j_pieces = j_pieces;
-  P->j_rounds = 0;
-  if (T.jframes) {
-    uint32_t r = 1;
-    while (r < (uint32_t)J_MAX_ROUNDS - 1 && (1ull << r) <= j_maxseq + 1) r++;
-    P->j_rounds = r + 1;
-  }
-  W.jblk = carve(sizeof(JBlk) * std::max<uint64_t>(T.jblk, 1));
-  W.jseg = carve(sizeof(JSeg) * std::max<uint64_t>(T.jseg, 1));
-  W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
-  W.jdone = carve(std::max<uint64_t>(j_pieces, 1));
-  W.jst = carve(4 * P->j_bytes + 64);
-  W.redo = carve(std::max<uint64_t>(T.frames, 1));
-  W.k2done = carve(4);
+  carve_tail(P, W, T, o, j_base, j_pieces, j_maxseq);
   W.total = o;
 
-  zd_plan_info& I = P->info;
-  I.nframes = T.frames;
-  I.nblocks = T.blocks;
-  I.ncompressed = T.comps;
-  I.out_bytes = T.out;
-  I.out_exact = T.exact;
-  I.workspace_bytes = W.total;
-  I.nsequences = T.nseq;
-  I.nliterals = T.lits;
-  I.index_status = P->index_status;
-  I.executors = (P->fused ? ZD_EXEC_FUSED : 0u) | (P->n_k4f ? ZD_EXEC_K4F : 0u) | (P->n_jframes ? ZD_EXEC_K4J : 0u);
+  plan_info(P, T);
   return 0;
 }
 
@@ -854,6 +660,15 @@ void ws_release(uint8_t* p, uint64_t bytes, int dev) {
   }
 }
 
+// the output staging of a plan whose frames' sizes are bounds
+int upload_staging(zd_plan* P) {
+  if (!P->info.out_exact) {
+    P->staging_bytes = P->info.out_bytes;
+    HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
+  }
+  return 0;
+}
+
 int upload_plan(zd_plan* P) {
   HIPCHK(hipGetDevice(&P->dev));
   HIPCHK(ws_alloc(P->dev, P->W.total, &P->d_ws, &P->ws_bytes));
@@ -882,11 +697,7 @@ int upload_plan(zd_plan* P) {
     for (const Piece& q : pieces)
       if (q.bytes) HIPCHK(hipMemcpy(P->d_ws + q.off, q.p, q.bytes, hipMemcpyHostToDevice));
   }
-  if (!P->info.out_exact) {
-    P->staging_bytes = P->info.out_bytes;
-    HIPCHK(hipMalloc(&P->d_staging, std::max<uint64_t>(P->staging_bytes, 16)));
-  }
-  return 0;
+  return upload_staging(P);
 }
 
 // A plan's second stream and its fork/join events, kept for the next plans
@@ -1087,6 +898,17 @@ struct DevWalkBufs {                      // device and pinned buffers, kept bet
   size_t cap_h = 0;
   WalkRange* h_wr = nullptr;             // pinned
   size_t cap_hwr = 0;
+  size_t fb = 0, bytes = 0;              // the last fill pass: frames | blocks layout in d_out
+  // the device descriptor build (build_plan_device): per-frame counts and
+  // tile sums, the frames' output offsets and capacities, the shape
+  uint64_t* d_cnt = nullptr;
+  size_t cap_cnt = 0;
+  uint64_t* d_tot = nullptr;
+  size_t cap_tot = 0;
+  uint64_t* d_fo = nullptr;
+  size_t cap_fo = 0;
+  PlanShape* d_shape = nullptr;
+  uint64_t* h_small = nullptr;           // pinned: shape, totals
 };
 DevWalkBufs& dev_walk_bufs() {
   static DevWalkBufs* b = new DevWalkBufs();
@@ -1195,10 +1017,21 @@ int io_d2h(uint8_t* h, const uint8_t* d, size_t n, hipStream_t s, IoRing& R, hip
   return 0;
 }
 
+// The fill pass's index (in B.d_out) -> the pinned copy
+int dev_walk_download(DevWalkBufs& B, hipStream_t s, const HostFrame** frames, const HostBlock** blocks) {
+  if (hipMemcpyAsync(B.h_out, B.d_out, B.bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return ZD_E_HIP;
+  *frames = (const HostFrame*)B.h_out;
+  *blocks = (const HostBlock*)(B.h_out + B.fb);
+  return 0;
+}
+
 // Walks `nranges` ranges from `first`; on return wr (pinned) holds the
 // summaries with f_off / b_off, frames / blocks (pinned) the fill pass.
 int dev_walk(DevWalkBufs& B, const uint8_t* d_src, uint64_t n, uint64_t first, uint64_t chunk, uint32_t nranges,
-             hipStream_t s, uint64_t* F_out, uint64_t* B_out, const HostFrame** frames, const HostBlock** blocks) {
+             hipStream_t s, uint64_t* F_out, uint64_t* B_out, const HostFrame** frames, const HostBlock** blocks,
+             bool download = true) {
   if (!grow_dev(B.d_wr, B.cap_wr, nranges) || !grow_pinned(B.h_wr, B.cap_hwr, nranges)) return ZD_E_HIP;
   if (launch_walk(d_src, n, first, chunk, nranges, B.d_wr, nullptr, nullptr, false, s) != hipSuccess ||
       hipMemcpyAsync(B.h_wr, B.d_wr, nranges * sizeof(WalkRange), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1217,13 +1050,12 @@ int dev_walk(DevWalkBufs& B, const uint8_t* d_src, uint64_t n, uint64_t first, u
   HostFrame* d_frames = (HostFrame*)B.d_out;
   HostBlock* d_blocks = (HostBlock*)(B.d_out + fb);
   if (hipMemcpyAsync(B.d_wr, B.h_wr, nranges * sizeof(WalkRange), hipMemcpyHostToDevice, s) != hipSuccess ||
-      launch_walk(d_src, n, first, chunk, nranges, B.d_wr, d_frames, d_blocks, true, s) != hipSuccess ||
-      hipMemcpyAsync(B.h_out, B.d_out, bytes, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
+      launch_walk(d_src, n, first, chunk, nranges, B.d_wr, d_frames, d_blocks, true, s) != hipSuccess)
     return ZD_E_HIP;
-  *frames = (const HostFrame*)B.h_out;
-  *blocks = (const HostBlock*)(B.h_out + fb);
-  return 0;
+  B.fb = fb;
+  B.bytes = bytes;
+  if (download) return dev_walk_download(B, s, frames, blocks);
+  return hipStreamSynchronize(s) != hipSuccess ? ZD_E_HIP : 0;
 }
 
 // Frames fr[i] (i in the kept list) with their blocks (global indices into
@@ -1251,6 +1083,83 @@ void parts_from(const std::vector<const HostFrame*>& kept, const HostBlock* bl, 
   });
 }
 
+// The descriptors of a device-walked plan built on the GPU:
+// frames [0, F) of the walk's index in B.d_out (block indices global) are the
+// plan's frames.  The host reads back the routing shape (two counters), the
+// plan's totals (PLAN_FIELDS words) and the frames' output offsets and
+// capacities (16 bytes a frame); everything else is written in place in the
+// workspace by the planner's own per-frame pass (zd_plan.h plan_frame).
+// Returns 1 when the plan needs the host's descriptors instead (K4J frames,
+// whose descriptors are listed in frame order on the host).
+int build_plan_device(zd_plan* P, DevWalkBufs& B, uint64_t F, hipStream_t s) {
+  const HostFrame* d_frames = (const HostFrame*)B.d_out;
+  const HostBlock* d_blocks = (const HostBlock*)(B.d_out + B.fb);
+  if (k4j_mode_of(P->flags) == 1) return 1;
+  P->nframes = F;
+  const uint32_t k4j_min = F <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
+  const uint64_t nt = (F + 255) / 256;
+  if (!B.d_shape && hipMalloc(&B.d_shape, sizeof(PlanShape)) != hipSuccess) return ZD_E_HIP;
+  if (!B.h_small && hipHostMalloc((void**)&B.h_small, 64 * 8, hipHostMallocDefault) != hipSuccess) return ZD_E_HIP;
+  if (!grow_dev(B.d_cnt, B.cap_cnt, std::max<uint64_t>(F, 1) * PLAN_FIELDS) ||
+      !grow_dev(B.d_tot, B.cap_tot, (nt + 1) * PLAN_FIELDS) || !grow_dev(B.d_fo, B.cap_fo, 2 * std::max<uint64_t>(F, 1)))
+    return ZD_E_HIP;
+  HIPCHK(launch_plan_shape(d_frames, F, k4j_min, B.d_shape, s));
+  HIPCHK(hipMemcpyAsync(B.h_small, B.d_shape, sizeof(PlanShape), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  PlanShape shape;
+  memcpy(&shape, B.h_small, sizeof shape);
+  const int32_t none[3] = {-1, -1, -1};
+  const uint64_t rep0[3] = {1, 4, 8};
+  const PlanCtx X = plan_ctx(P, -1, none, 0, rep0, 0, shape.multi == 0, k4j_mode_of(P->flags) < 0 ? shape.jcand : 0);
+  if (X.k4j_auto) return 1;                     // some frame goes to K4J
+  HIPCHK(launch_plan_count(X, d_frames, d_blocks, F, B.d_cnt, B.d_tot, s));
+  HIPCHK(hipMemcpyAsync(B.h_small, B.d_tot + nt * PLAN_FIELDS, PLAN_FIELDS * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  PlanCounts T;
+  memcpy(&T, B.h_small, sizeof T);
+  if (T.jframes) return 1;
+  Workspace& W = P->W;
+  W = Workspace{};
+  uint64_t o = 0;
+  carve_head(W, T, o);
+  P->desc_bytes = o;
+  plan_totals(P, T, X.fused);
+  carve_tail(P, W, T, o, 0, 0, 0);
+  W.hframes = o;
+  o = align_up(o + sizeof(HostFrame) * std::max<uint64_t>(F, 1), 256);
+  W.total = o;
+  HIPCHK(hipGetDevice(&P->dev));
+  HIPCHK(ws_alloc(P->dev, W.total, &P->d_ws, &P->ws_bytes));
+  uint8_t* b = P->d_ws;
+  uint64_t* d_fout = B.d_fo;
+  uint64_t* d_fcap = B.d_fo + std::max<uint64_t>(F, 1);
+  const Sink S{(CompBlock*)(b + W.comp), (BlockRec*)(b + W.blocks), (FrameDesc*)(b + W.frames),
+               (FrameState*)(b + W.frame_state0), (uint32_t*)(b + W.list_tables), (uint32_t*)(b + W.list_huf),
+               (uint32_t*)(b + W.list_seq), (uint32_t*)(b + W.list_k4f), (CopyDesc*)(b + W.copies),
+               (JFrame*)(b + W.jframes), (JBlkDesc*)(b + W.jblkd), (JSegDesc*)(b + W.jsegd), d_fout, d_fcap};
+  HIPCHK(launch_plan_fill(X, d_frames, d_blocks, F, B.d_cnt, B.d_tot, S, s));
+  if (F) HIPCHK(hipMemcpyAsync(b + W.hframes, d_frames, F * sizeof(HostFrame), hipMemcpyDeviceToDevice, s));
+  P->frame_out.resize(F);
+  P->frame_cap.resize(F);
+  if (F) {
+    HIPCHK(hipMemcpyAsync(P->frame_out.data(), d_fout, F * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(P->frame_cap.data(), d_fcap, F * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  P->dev_built = true;
+  P->staged = false;
+  plan_info(P, T);
+  P->info.device_descriptors = 1;
+  return 0;
+}
+
+// ZD_DEV_DESC=0 (read once): device-walked plans take the host's descriptor
+// build (the comparison leg of tests/test_gpu_walk.py)
+bool dev_host_descriptors() {
+  static const bool off = getenv("ZD_DEV_DESC") && atoi(getenv("ZD_DEV_DESC")) == 0;
+  return off;
+}
+
 int plan_index_dev(zd_plan* P, const uint8_t* d_src, size_t n, hipStream_t s) {
   const auto tw0 = std::chrono::steady_clock::now();
   std::vector<HostPart> keep;
@@ -1273,9 +1182,43 @@ int plan_index_dev(zd_plan* P, const uint8_t* d_src, size_t n, hipStream_t s) {
     uint64_t F = 0, NB = 0;
     const HostFrame* fr = nullptr;
     const HostBlock* bl = nullptr;
-    if (int r = dev_walk(B, d_src, n, 0, chunk, T, s, &F, &NB, &fr, &bl)) return r;
+    if (int r = dev_walk(B, d_src, n, 0, chunk, T, s, &F, &NB, &fr, &bl, false)) return r;
     t_walk = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
     const auto cut = [&](size_t k) { return std::min<uint64_t>((uint64_t)k * chunk, n); };
+    // The common case from the range summaries alone: every range's chain
+    // starts where the kept frames before it end (or the range lies inside a
+    // kept frame and found none), so the plan's frames are a prefix of the
+    // walk's index, and its descriptors are built where the index is
+    // (build_plan_device); otherwise the index comes back for the host stitch.
+    if (F && !dev_host_descriptors()) {
+      uint64_t cur = 0, kept_end = 0;
+      int st = 0;
+      bool ok = true;
+      for (size_t k = 0; k < T && !st && ok; k++) {
+        const WalkRange& R = B.h_wr[k];
+        if (k && cur >= cut(k + 1)) { ok = R.nframes == 0; continue; }
+        if (k && !(R.nframes && R.p0 == cur)) { ok = false; break; }
+        kept_end = R.f_off + R.nframes;
+        st = R.status;
+        cur = R.end;
+      }
+      if (ok) {
+        const int r = build_plan_device(P, B, kept_end, s);
+        if (r < 0) return r;
+        if (r == 0) {
+          P->index_status = st;
+          P->info.index_status = st;
+          P->info.walk_serial_bytes = 0;
+          P->index_stop = P->nframes;
+          if (getenv("ZD_PLAN_TIMES"))
+            fprintf(stderr, "zd device walk + descriptors: %.2f ms (walk %.2f)\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count(), t_walk);
+          return 0;
+        }
+      }
+    }
+    if (F)
+      if (int r = dev_walk_download(B, s, &fr, &bl)) return r;
     struct Chain {                                   // one range's frames
       const HostFrame* p; size_t n;
       size_t size() const { return n; }
@@ -1361,7 +1304,14 @@ static void dump_plan_desc(const zd_plan* P) {
   if (!f) return;
   auto w = [&](const void* p, size_t bytes) { uint64_t b = bytes; fwrite(&b, 8, 1, f); if (bytes) fwrite(p, 1, bytes, f); };
   const Workspace& W = P->W;
+  std::vector<uint8_t> dev_head;               // a device-built plan's descriptors, read back
+  if (P->dev_built) {
+    dev_head.resize(P->desc_bytes);
+    if (P->desc_bytes && hipMemcpy(dev_head.data(), P->d_ws, P->desc_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      (void)hipGetLastError();
+  }
   auto at = [&](uint64_t off, const void* vec) -> const void* {
+    if (P->dev_built) return (const void*)(dev_head.data() + off);
     return P->staged ? (const void*)(host_stage().p + off) : vec;
   };
   w(at(W.comp, P->comps.data()), P->n_comps * sizeof(CompBlock));
@@ -1378,6 +1328,7 @@ static void dump_plan_desc(const zd_plan* P) {
   w(at(W.jsegd, P->jsegd.data()), P->n_jseg * sizeof(JSegDesc));
   w(P->frame_out.data(), P->frame_out.size() * 8);
   zd_plan_info I = P->info; I.workspace_bytes = 0; I.host_ns = I.device_ns = 0; I.walk_serial_bytes = 0;
+  I.device_descriptors = 0;
   w(&I, sizeof I);
   uint64_t x[4] = {P->j_bytes, P->j_pieces, P->j_rounds, (uint64_t)(int64_t)P->index_status};
   w(x, sizeof x);
@@ -1534,7 +1485,8 @@ static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint3
   const auto ti = std::chrono::steady_clock::now();
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {1, 4, 8};
-  if (int r = build_plan(P, -1, none, 0, rep0, 0, true)) { zd_plan_destroy(P); return r; }
+  if (!P->dev_built)
+    if (int r = build_plan(P, -1, none, 0, rep0, 0, true)) { zd_plan_destroy(P); return r; }
   P->info.src_bytes = n;
   const auto t1 = std::chrono::steady_clock::now();
   dump_plan_desc(P);
@@ -1542,7 +1494,7 @@ static int plan_create(const uint8_t* src, const uint8_t* d_src, size_t n, uint3
     fprintf(stderr, "zd plan: index %.2f ms, descriptors %.2f ms\n",
             std::chrono::duration<double, std::milli>(ti - t0).count(),
             std::chrono::duration<double, std::milli>(t1 - ti).count());
-  int r = upload_plan(P);
+  int r = P->dev_built ? upload_staging(P) : upload_plan(P);
   const auto tu = std::chrono::steady_clock::now();
   // the second stream and its events (K2 beside K3) exist
   // from here on, so zd_decode_async creates nothing

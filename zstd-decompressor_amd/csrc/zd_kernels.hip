@@ -4401,6 +4401,114 @@ __global__ __launch_bounds__(64) void zd_k_walk(const uint8_t* __restrict__ src,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Device descriptors (zd_plan_create_device): the planner's
+// per-frame pass (zd_plan.h plan_frame, the host planner's own code) over the
+// device walk's frame / block index, one lane per frame.  A shape pass (the
+// plan-wide inputs of routing: frames that are not single-block zstd frames,
+// K4J candidates), a count pass (each frame's PlanCounts from zero), an
+// exclusive scan over frames (per 256-frame tile, then the tiles), and a fill
+// pass that writes CompBlock / BlockRec / FrameDesc / FrameState, the work
+// lists and K0's pieces straight into the plan's workspace.  Only the plan's
+// totals and the frames' output offsets and capacities go back to the host.
+// ---------------------------------------------------------------------------
+struct DevJNone {            // K4J frames are listed by the host planner only
+  __device__ void push_back(uint32_t) {}
+};
+__global__ __launch_bounds__(256) void zd_k_plan_shape(const HostFrame* __restrict__ frames, uint64_t nf,
+                                                       uint32_t k4j_min, PlanShape* out) {
+  const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  bool multi = false, jc = false;
+  if (f < nf) {
+    const HostFrame& hf = frames[f];
+    multi = hf.d.kind != ZD_FRAME_ZSTD || hf.key != KEY_NONE || hf.nb != 1;
+    jc = hf.key == KEY_NONE && hf.ncomp >= k4j_min;
+  }
+  const uint32_t m = (uint32_t)__popcll(__ballot(multi)), j = (uint32_t)__popcll(__ballot(jc));
+  if ((threadIdx.x & 63) == 0) {
+    if (m) atomicAdd(&out->multi, m);
+    if (j) atomicAdd(&out->jcand, j);
+  }
+}
+__global__ __launch_bounds__(256) void zd_k_plan_count(PlanCtx X, const HostFrame* __restrict__ frames,
+                                                       const HostBlock* __restrict__ blocks, uint64_t nf,
+                                                       PlanCounts* cnt) {
+  const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= nf) return;
+  PlanCounts c{};
+  const Sink none{};
+  plan_frame<false, DevJNone>(X, frames[f], blocks, c, none, nullptr);
+  cnt[f] = c;
+}
+// Exclusive scan of the PlanCounts words over frames, in place: tile t's
+// words (256 frames) scanned in LDS, its totals to tot[t]; then one
+// workgroup scans the tiles (lane j: word j); then every frame adds its
+// tile's start.  tot[ntiles] = the plan's totals.
+__global__ __launch_bounds__(256) void zd_k_plan_scan_tiles(uint64_t* cnt, uint64_t nf, uint64_t* tot) {
+  __shared__ uint64_t s[256];
+  const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int w = 0; w < PLAN_FIELDS; w++) {
+    const uint64_t v = f < nf ? cnt[f * PLAN_FIELDS + w] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+      const uint64_t a = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0;
+      __syncthreads();
+      s[threadIdx.x] += a;
+      __syncthreads();
+    }
+    if (f < nf) cnt[f * PLAN_FIELDS + w] = s[threadIdx.x] - v;    // exclusive within the tile
+    if (threadIdx.x == 255) tot[(uint64_t)blockIdx.x * PLAN_FIELDS + w] = s[255];
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(64) void zd_k_plan_scan_sums(uint64_t* tot, uint64_t ntiles) {
+  const int w = threadIdx.x;
+  if (w >= PLAN_FIELDS) return;
+  uint64_t acc = 0;
+  for (uint64_t t = 0; t < ntiles; t++) {
+    const uint64_t v = tot[t * PLAN_FIELDS + w];
+    tot[t * PLAN_FIELDS + w] = acc;
+    acc += v;
+  }
+  tot[ntiles * PLAN_FIELDS + w] = acc;
+}
+__global__ __launch_bounds__(256) void zd_k_plan_fill(PlanCtx X, const HostFrame* __restrict__ frames,
+                                                      const HostBlock* __restrict__ blocks, uint64_t nf,
+                                                      const uint64_t* __restrict__ cnt, const uint64_t* __restrict__ tot,
+                                                      Sink S) {
+  const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= nf) return;
+  PlanCounts c;
+  uint64_t* cw = (uint64_t*)&c;
+  for (int w = 0; w < PLAN_FIELDS; w++) cw[w] = cnt[f * PLAN_FIELDS + w] + tot[(uint64_t)blockIdx.x * PLAN_FIELDS + w];
+  plan_frame<true, DevJNone>(X, frames[f], blocks, c, S, nullptr);
+}
+
+hipError_t launch_plan_shape(const HostFrame* frames, uint64_t nf, uint32_t k4j_min, PlanShape* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(PlanShape), s);
+  if (e != hipSuccess) return e;
+  if (nf) hipLaunchKernelGGL(zd_k_plan_shape, dim3((uint32_t)((nf + 255) / 256)), dim3(256), 0, s, frames, nf, k4j_min, out);
+  return hipGetLastError();
+}
+hipError_t launch_plan_count(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
+                             uint64_t* cnt, uint64_t* tot, hipStream_t s) {
+  const uint32_t nt = (uint32_t)((nf + 255) / 256);
+  if (nf) {
+    hipLaunchKernelGGL(zd_k_plan_count, dim3(nt), dim3(256), 0, s, X, frames, blocks, nf, (PlanCounts*)cnt);
+    hipLaunchKernelGGL(zd_k_plan_scan_tiles, dim3(nt), dim3(256), 0, s, cnt, nf, tot);
+  }
+  hipLaunchKernelGGL(zd_k_plan_scan_sums, dim3(1), dim3(64), 0, s, tot, (uint64_t)nt);
+  return hipGetLastError();
+}
+hipError_t launch_plan_fill(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
+                            const uint64_t* cnt, const uint64_t* tot, const Sink& S, hipStream_t s) {
+  if (nf)
+    hipLaunchKernelGGL(zd_k_plan_fill, dim3((uint32_t)((nf + 255) / 256)), dim3(256), 0, s, X, frames, blocks, nf, cnt,
+                       tot, S);
+  return hipGetLastError();
+}
+
 hipError_t launch_walk(const uint8_t* src, uint64_t n, uint64_t first, uint64_t chunk, uint32_t nranges, WalkRange* wr,
                        HostFrame* frames, HostBlock* blocks, bool fill, hipStream_t s) {
   if (!nranges) return hipSuccess;

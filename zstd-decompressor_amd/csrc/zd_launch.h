@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "zd_common.h"
+#include "zd_plan.h"
 
 namespace zd {
 
@@ -52,8 +53,19 @@ struct HostBlock;
 hipError_t launch_walk(const uint8_t* src, uint64_t n, uint64_t first, uint64_t chunk, uint32_t nranges, WalkRange* wr,
                        HostFrame* frames, HostBlock* blocks, bool fill, hipStream_t s);
 
+// Device descriptors (zd_plan_create_device): the shape pass (PlanShape
+// zeroed first), the count pass + exclusive scan (cnt: nf x PLAN_FIELDS
+// words, scanned within 256-frame tiles; tot: (tiles + 1) x PLAN_FIELDS
+// words, the tiles' starts and then the plan's totals), the fill pass.
+struct PlanShape { uint32_t multi, jcand; };
+hipError_t launch_plan_shape(const HostFrame* frames, uint64_t nf, uint32_t k4j_min, PlanShape* out, hipStream_t s);
+hipError_t launch_plan_count(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
+                             uint64_t* cnt, uint64_t* tot, hipStream_t s);
+hipError_t launch_plan_fill(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
+                            const uint64_t* cnt, const uint64_t* tot, const Sink& S, hipStream_t s);
+
 constexpr int N_KERNELS = 6;
-constexpr uint32_t K4F_CAP = 128u << 10;   // frames up to this output size execute in LDS (K4F)
+constexpr uint32_t K4F_CAP = K4F_CAP_BYTES;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];
 
 }  // namespace zd

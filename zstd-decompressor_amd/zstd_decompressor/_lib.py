@@ -46,7 +46,7 @@ class PlanInfo(C.Structure):
                 ("device_ns", C.c_uint64), ("walk_serial_bytes", C.c_uint64),
                 ("io_h2d_ns", C.c_uint64), ("io_decode_ns", C.c_uint64), ("io_d2h_ns", C.c_uint64),
                 ("error_key", C.c_uint64), ("replans", C.c_uint64),
-                ("fused_redo_frames", C.c_uint64)]
+                ("fused_redo_frames", C.c_uint64), ("device_descriptors", C.c_uint64)]
 
 
 class GatherResult(C.Structure):
