@@ -951,15 +951,246 @@ static_assert(K2_LANES <= 64, "K2 workgroup must be a single wave");
 static_assert(K2_GROUP * LUT_MAX_BITS <= 97, "a group must fit one window");
 static_assert((K2_GROUP / 2) * LUT_MAX_BITS <= 64, "half a group must fit 64 bits");
 typedef __attribute__((address_space(1))) uint64_t g_u64a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) u64x2a1 gw_u64x2a1;
+
+// ---------------------------------------------------------------------------
+// K2's pair table.  Trees of maxBits p <= 11 are decoded through a table of
+// u32 entries, each giving the symbols a bit prefix starts with -- two when
+// both codes fit the prefix -- so K2's serial chain (LDS lookup, shift) runs
+// once per 1.6-1.8 symbols on zstd's literals instead of once per symbol.
+// zd_k_huf_pairs converts a block's u16 LUT (K1) into it, in place in the LUT
+// slot.  Prefixes are 10 bits, except that the lowest L 10-bit prefixes --
+// those whose first code is 11 bits: insert places the longest codes first
+// (huffman.rs:132-175), so they are the leading ones -- are split into their
+// two 11-bit prefixes.  With x the top 11 bits of the window the entry is
+//   j = min(x, (x >> 1) + L)
+// (x for x >> 1 < L, the 10-bit prefix + L past them), 1024 + L entries.
+//   bits 0-4   (32 - bits consumed) & 31      (v_alignbit takes it as is)
+//   bits 5-7   0      bit 8  PR_TWO: a second symbol      bits 9-10  0
+//              (K2 sums a half's four entries: bits 0-7 give its bits,
+//              bits 8-10 its second symbols)
+//   bits 11-14 width of the first code (PR_BAD: the absent node's depth;
+//              0 with PR_BAD: PR_LONG, below)
+//   bit 15     PR_BAD: K2's fast loop stops (absent node, or PR_LONG)
+//   bits 16-23 first symbol             bits 24-31 second symbol (or 0)
+// A deep 10-bit prefix past the leading run (only a malformed tree's last
+// gap) is PR_LONG: the symbols of its 11-bit prefixes 0 / 1 in bits 16-23 /
+// 24-31, bit 5 / 6 set when that node is absent (the exact path decodes it).
+// ---------------------------------------------------------------------------
+constexpr uint32_t PR_TWO = 1u << 8, PR_BAD = 1u << 15, PR_BAD0 = 1u << 5, PR_BAD1 = 1u << 6;
+constexpr int PR_BITS = 10;
+constexpr uint32_t PR_LMAX = 128;                  // split prefixes: n11 <= 256 codes of 11 bits, + a hole
+constexpr uint32_t PR_ENTRIES = (1u << PR_BITS) + PR_LMAX;
+constexpr uint32_t PR_L_AT = PR_ENTRIES;           // u32 index of L in the slot
+static_assert((PR_L_AT + 1) * 4 <= LUT_ENTRIES * 2, "a pair table fits its LUT slot");
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) const uint32_t gc_u32;
+
+__device__ inline uint32_t pr_index(uint32_t x, uint32_t L) { return min(x, (x >> 1) + L); }
+
+// The entry of the nb-bit prefix x (nb 10 or 11, p <= 11, the first code no
+// longer than nb) from the u16 LUT (decode entries of the p-bit prefix,
+// lut_field's (32 - f) form).
+__device__ inline uint32_t pr_entry(const lds_u16* u, int p, uint32_t x, int nb) {
+  auto at = [&](uint32_t y) { return p >= nb ? y << (p - nb) : y >> (nb - p); };
+  const uint32_t e1 = u[at(x)];
+  const uint32_t w1 = lut_width(e1, true);
+  if (e1 & LUT_ABSENT) return PR_BAD | w1 << 11;
+  uint32_t total = w1, two = 0, s2 = 0;
+  if (w1 < (uint32_t)nb) {
+    const uint32_t e2 = u[at((x << w1) & ((1u << nb) - 1))];
+    const uint32_t w2 = lut_width(e2, true);
+    if (!(e2 & LUT_ABSENT) && w2 <= nb - w1) {
+      total += w2;
+      two = PR_TWO;
+      s2 = e2 & 0xFF;
+    }
+  }
+  return ((32u - total) & 31) | two | w1 << 11 | (e1 & 0xFF) << 16 | s2 << 24;
+}
+
+// One symbol of the p-bit prefix idx (p <= 11) from a pair table, as the u16
+// LUT gives it: the symbol, *nb its width (an absent node: its depth, *absent).
+template <typename TP>
+__device__ inline uint32_t pr_one(TP dl, uint32_t L, int p, uint32_t idx, int32_t* nb, bool* absent) {
+  const uint32_t x = idx << (11 - p);
+  const uint32_t e = dl[pr_index(x, L)];
+  const uint32_t w = (e >> 11) & 15;
+  if ((e & PR_BAD) && w == 0) {                   // PR_LONG
+    const uint32_t b = x & 1;
+    *nb = 11;
+    *absent = (e & (b ? PR_BAD1 : PR_BAD0)) != 0;
+    return (e >> (16 + 8 * b)) & 0xFF;
+  }
+  *nb = (int32_t)w;
+  *absent = (e & PR_BAD) != 0;
+  return (e >> 16) & 0xFF;
+}
+
+// zd_k_huf_pairs: one wave per block of K1's list that built a LUT of maxBits
+// <= 11: the LUT is staged in LDS, L found by a wave reduction, then the
+// slot is overwritten with the pair table and L.
+constexpr int PR_WAVES = 4;
+__global__ __launch_bounds__(64 * PR_WAVES) void zd_k_huf_pairs(const CompBlock* __restrict__ comp,
+                                                                 const CompState* __restrict__ cstate,
+                                                                 const uint32_t* __restrict__ list, uint32_t n_list,
+                                                                 uint16_t* luts) {
+  __shared__ __attribute__((aligned(16))) uint16_t u[PR_WAVES][1 << K2_LUT_BITS];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t li = blockIdx.x * PR_WAVES + wv;
+  if (li >= n_list) return;                        // whole waves: no workgroup barrier below
+  const uint32_t ci = list[li];
+  const CompBlock& C = comp[ci];
+  if (C.lit_type != LIT_COMPRESSED || C.host_stage <= PS_HUF_DESC || C.prebuilt) return;
+  const int p = cstate[ci].huf_bits;
+  if (p == 0 || p > K2_LUT_BITS) return;
+  uint16_t* slot = luts + (uint64_t)C.lut_slot * LUT_ENTRIES;
+  const lds_u16* U = (const lds_u16*)u[wv];
+  {                                                // 16 bytes per lane and step
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const int n16 = (1 << p) / 8;
+    if (n16 == 0) { if (lane < (1 << p)) u[wv][lane] = slot[lane]; }
+    else for (int e = lane; e < n16; e += 64) ((u32x4*)u[wv])[e] = ((const u32x4*)slot)[e];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // deep(i): the 10-bit prefix i starts with an 11-bit code or absent node
+  auto deep = [&](uint32_t i) {
+    return p > PR_BITS && (lut_width(U[2 * i], true) > PR_BITS || lut_width(U[2 * i + 1], true) > PR_BITS);
+  };
+  uint32_t first = 1u << PR_BITS;                  // the lowest prefix that is not deep
+  for (uint32_t i = lane; i < (1u << PR_BITS); i += 64)
+    if (!deep(i)) { first = i; break; }
+  for (int o = 32; o > 0; o >>= 1) first = min(first, (uint32_t)__shfl_xor((int)first, o));
+  const uint32_t L = min(first, PR_LMAX);
+  uint32_t* dl = (uint32_t*)slot;
+  for (uint32_t j = lane; j < (1u << PR_BITS) + L; j += 64) {
+    uint32_t ent;
+    if (j < 2 * L) {
+      ent = pr_entry(U, p, j, 11);
+    } else {
+      const uint32_t i = j - L;
+      if (deep(i)) {                               // PR_LONG
+        const uint32_t e0 = U[2 * i], e1 = U[2 * i + 1];
+        ent = PR_BAD | (e0 & 0xFF) << 16 | (e1 & 0xFF) << 24 | ((e0 & LUT_ABSENT) ? PR_BAD0 : 0u) |
+              ((e1 & LUT_ABSENT) ? PR_BAD1 : 0u);
+      } else {
+        ent = pr_entry(U, p, i, PR_BITS);
+      }
+    }
+    dl[j] = ent;
+  }
+  if (lane == 0) dl[PR_L_AT] = L;
+}
+
+// One Huffman stream of a tree of maxBits p <= 11 from its pair table (LDS,
+// or HBM for a workgroup with a deeper tree; huffman.rs:205-218 on a
+// BackwardBitParser, parsing.rs:191-259).  Fast path while at least
+// K2_GROUP * 12 bits remain: 24-byte windows two groups ahead (the window
+// loaded when group g ends, ending at the byte of pos_{g+1}, covers groups
+// g+1 and g+2, so a load has a whole group more to land); a group is two
+// halves of 4 lookups (<= 44 bits each, 4-8 symbols), one 8-byte store per
+// half at the half's first byte (its bytes past the half's symbols are
+// overwritten by what follows).  Both groups of a trip run on every lane; a
+// lane that stops keeps its position and stores into the slack.  The tail
+// (and any group that meets PR_BAD) goes symbol by symbol with the
+// reference's checks.
+template <typename TP>
+__device__ int huf_stream_pr(const uint8_t* bs, uint32_t size, uintptr_t base, TP dl, uint32_t L, int p,
+                             uint8_t* out, uint32_t cap, uint32_t* count_out, uint8_t* dummy) {
+  uint32_t count = 0;
+  *count_out = 0;
+  if (size == 0) return ZD_E_EMPTY_INPUT_DATA;
+  const uint8_t lastb = bs[size - 1];
+  if (lastb == 0) return ZD_E_NULL_BYTE;
+  int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
+  constexpr uint32_t ROOM = 2 * K2_GROUP;          // the bytes a group's two stores may touch
+  const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-24);
+  Win6 wa = win6_load(bs, m, pos);
+  asm volatile("" ::: "memory");
+  *(g_u64a1*)dummy = 0;
+  Win6 wb = win6_load(bs, m, pos);
+  asm volatile("" ::: "memory");
+  *(g_u64a1*)dummy = 0;
+  bool live = pos >= K2_GROUP * LUT_MAX_BITS && count + ROOM <= cap;
+  auto group = [&](Win6& w) {
+    uint64_t acc[2];
+    uint32_t n[2], used = 0, bad = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint64_t t = win6_top64(w, pos - (int32_t)used);
+      uint32_t hi = (uint32_t)(t >> 32), lo = (uint32_t)t, S = 0;
+      uint64_t a = 0;
+#pragma unroll
+      for (int j = 0; j < K2_GROUP / 2; j++) {
+        const uint32_t e = dl[pr_index(hi >> 21, L)];
+        hi = __builtin_amdgcn_alignbit(hi, lo, e);
+        lo = __builtin_amdgcn_alignbit(lo, 0u, e);
+        const uint32_t c8 = 8 * j + 8 * ((S >> 8) & 7);          // bytes before this lookup's
+        a |= (uint64_t)(e >> 16) << c8;
+        S += e;
+        bad |= e;
+      }
+      used += 32 * (K2_GROUP / 2) - (S & 0xFF);
+      acc[h] = a;
+      n[h] = K2_GROUP / 2 + ((S >> 8) & 7);
+    }
+    const bool ok = live && !(bad & PR_BAD);
+    pos = ok ? pos - (int32_t)used : pos;
+    w = win6_load(bs, m, pos);
+    asm volatile("" ::: "memory");
+    // the group's bytes as one 16-byte store: half 1's after half 0's n[0]
+    // (4..8); bytes past a half's symbols are 0
+    const uint32_t s0 = 8 * n[0] - 32;                      // 0..32
+    const uint64_t v0 = acc[0] | ((acc[1] << s0) << 32);
+    const uint64_t v1 = s0 == 32 ? acc[1] : acc[1] >> (32 - s0);
+#ifdef ZD_EXP_K2_NOSTORE                           // experiment: the literals are not stored (wrong output)
+    *(g_u64a1*)dummy = v0 ^ v1;
+#else
+    *(gw_u64x2a1*)(ok ? out + count : dummy) = (u64x2a1){v0, v1};
+#endif
+    count += ok ? n[0] + n[1] : 0;
+    live = ok && pos >= K2_GROUP * LUT_MAX_BITS && count + ROOM <= cap;
+  };
+  while (live) {
+    group(wa);
+    group(wb);
+  }
+  // symbol by symbol with the reference's checks (huf_stream's tail)
+  int st = 0;
+  WinU w = winu_load(bs, base, pos);
+  int32_t p0 = pos;
+  const uint32_t sh = 64 - p;
+  while (pos > 0 && !st) {
+    if ((p0 - pos) + (int32_t)w.sh > 100) {
+      w = winu_load(bs, base, pos);
+      p0 = pos;
+    }
+    uint32_t idx = (uint32_t)(winu_top(w, (uint32_t)(p0 - pos)) >> sh);
+    if (pos < p) idx &= ~((1u << (p - pos)) - 1);     // zero-fill below the stream (parsing.rs peek)
+    int32_t nb;
+    bool absent;
+    const uint32_t sym = pr_one(dl, L, p, idx, &nb, &absent);
+    if (absent) st = nb <= pos ? ZD_E_REF_PANIC : ZD_E_NOT_ENOUGH_BITS;
+    else if (nb > pos) st = ZD_E_NOT_ENOUGH_BITS;
+    else {
+      pos -= nb;
+      if (count < cap) out[count] = (uint8_t)sym;
+      count++;
+    }
+  }
+  *count_out = count;
+  return st;
+}
 
 // One Huffman stream, backward (huffman.rs:205-218 on a BackwardBitParser,
-// parsing.rs:191-259).  Fast path while at least K2_GROUP * 12 bits remain:
+// parsing.rs:191-259), LUT in HBM: a workgroup with a tree deeper than K2's
+// LDS tables (maxBits 12).  Fast path while at least K2_GROUP * 12 bits remain:
 // a byte-aligned 16-byte window per group of 8 symbols, the top 64 bits
-// taken twice (4 symbols each, <= 48 bits), one LDS lookup and one shift per
+// taken twice (4 symbols each, <= 48 bits), one lookup and one shift per
 // symbol, one 8-byte store per group.  The tail (and any group that meets an
 // absent tree node) goes symbol by symbol with the reference's checks.
-template <typename LP>
-__device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP lut, int p, uint8_t* out,
+__device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, g_u16* lut, int p, uint8_t* out,
                           uint32_t cap, uint32_t* count_out, uint8_t* dummy) {
   uint32_t count = 0;
   *count_out = 0;
@@ -968,57 +1199,11 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, LP l
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
   const uint32_t sh = 64 - p;
-  if constexpr (std::is_same<LP, const lds_u16*>::value) {
-    // LDS LUT (maxBits <= 11, a group reads <= 88 bits): 24-byte windows
-    // two groups ahead.  The window loaded when group g ends (ending at the
-    // byte of pos_{g+1}) covers groups g+1 and g+2, so group g+2 reads it and
-    // a load has a whole group more to land.  Both groups of a trip run on
-    // every lane; a lane that stops keeps its position (the tail redoes an
-    // absent-node group with the exact checks) and stores into the slack.
-    const int32_t m = (int32_t)max((intptr_t)base - (intptr_t)bs, (intptr_t)-24);
-    Win6 wa = win6_load(bs, m, pos);
-    asm volatile("" ::: "memory");
-    *(g_u64a1*)dummy = 0;
-    Win6 wb = win6_load(bs, m, pos);
-    asm volatile("" ::: "memory");
-    *(g_u64a1*)dummy = 0;
-    bool live = pos >= K2_GROUP * LUT_MAX_BITS && count + K2_GROUP <= cap;
-    auto group = [&](Win6& w) {
-      uint64_t acc = 0;
-      uint32_t used = 0, bad = 0;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const uint64_t t = win6_top64(w, pos - (int32_t)used);
-        uint32_t hi = (uint32_t)(t >> 32), lo = (uint32_t)t, ssum = 0;
-#pragma unroll
-        for (int j = 0; j < K2_GROUP / 2; j++) {
-          const uint32_t e = lut[hi >> (sh - 32)];
-          const uint32_t sf = e >> 8;                 // 32 - width (and the absent flag, bit 7)
-          bad |= e & LUT_ABSENT;
-          hi = __builtin_amdgcn_alignbit(hi, lo, sf);
-          lo = __builtin_amdgcn_alignbit(lo, 0u, sf);
-          ssum += sf & 31;
-          acc |= (uint64_t)(e & 0xFF) << (8 * (h * (K2_GROUP / 2) + j));
-        }
-        used += 32 * (K2_GROUP / 2) - ssum;
-      }
-      const bool ok = live && !bad;
-      pos = ok ? pos - (int32_t)used : pos;
-      w = win6_load(bs, m, pos);
-      asm volatile("" ::: "memory");
-      *(g_u64a1*)(ok ? out + count : dummy) = acc;
-      count += ok ? K2_GROUP : 0;
-      live = ok && pos >= K2_GROUP * LUT_MAX_BITS && count + K2_GROUP <= cap;
-    };
-    while (live) {
-      group(wa);
-      group(wb);
-    }
-  } else {
   // The next group's window is loaded before this group's store: vmcnt
   // drains in issue order, so a group waits for its window, not the store.
   // The loop entry repeats that order (a store into the block's literal
   // slack, never read) so the wait at the loop head stays vmcnt(1).
+  {
   WinU w = winu_load(bs, base, pos);
   asm volatile("" ::: "memory");
   *(g_u64a1*)dummy = 0;
@@ -1130,7 +1315,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
                                                          FrameState* fstate, const uint32_t* __restrict__ list,
                                                          uint32_t n_list, const uint16_t* __restrict__ luts,
                                                          uint8_t* lits, uint32_t* k2done) {
-  __shared__ __attribute__((aligned(16))) uint16_t lut[K2_BLOCKS][1 << K2_LUT_BITS];
+  __shared__ __attribute__((aligned(16))) uint32_t dl[K2_BLOCKS][PR_ENTRIES];
   __shared__ uint32_t counts[K2_BLOCKS][4];
   __shared__ int errs[K2_BLOCKS][4];
   const int lane = threadIdx.x, b = lane >> 2, k = lane & 3;
@@ -1155,14 +1340,14 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     }
   }
   const bool use_lds = __ballot(act && p > K2_LUT_BITS) == 0;
-  if (use_lds && act) {      // the block's 4 lanes copy its LUT, 16 bytes at a time
+  if (use_lds && act) {      // the block's 4 lanes copy its pair table, 16 bytes at a time
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const u32x4 g_u4;
     typedef __attribute__((address_space(3))) u32x4 l_u4;
-    const int n16 = (1 << p) / 8;
-    if (n16 == 0) { if (k == 0) for (int e = 0; e < (1 << p); e++) lut[b][e] = g[e]; }
-    else for (int e = k; e < n16; e += 4) ((l_u4*)lut[b])[e] = ((g_u4*)g)[e];
+#pragma unroll 4
+    for (int e = k; e < (int)PR_ENTRIES / 4; e += 4) ((l_u4*)dl[b])[e] = ((g_u4*)g)[e];
   }
+  const uint32_t L = act && p <= K2_LUT_BITS ? ((const uint32_t*)g)[PR_L_AT] : 0;
   __syncthreads();
   const int m = act ? C.nstreams : 0;
   const uint32_t R = act ? C.lit_regen : 0;
@@ -1175,7 +1360,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint8_t* blk = src + C.src;
     const uintptr_t lo = (uintptr_t)src;
     // the block's literal slot: R + 16 + lit_extra bytes of literals (the
-    // streams laid back-to-back may run past R), then 8 bytes of slack that
+    // streams laid back-to-back may run past R), then 16 bytes of slack that
     // the fast loops' placeholder stores hit (never read)
     uint8_t* slack = lits + C.lit_out + R + 16 + C.lit_extra;
     uint32_t count;
@@ -1184,10 +1369,13 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
       st = huf_stream_deep(blk + off, C.stream_size[k], lo, (const uint32_t*)g, p, lits + C.lit_out + start, cap,
                            &count);
     else if (use_lds)
-      st = huf_stream<const lds_u16*>(blk + off, C.stream_size[k], lo, (const lds_u16*)lut[b], p,
-                                      lits + C.lit_out + start, cap, &count, slack);
+      st = huf_stream_pr<const lds_u32*>(blk + off, C.stream_size[k], lo, (const lds_u32*)dl[b], L, p,
+                                         lits + C.lit_out + start, cap, &count, slack);
+    else if (p <= K2_LUT_BITS)
+      st = huf_stream_pr<gc_u32*>(blk + off, C.stream_size[k], lo, (gc_u32*)g, L, p, lits + C.lit_out + start, cap,
+                                 &count, slack);
     else
-      st = huf_stream<g_u16*>(blk + off, C.stream_size[k], lo, (g_u16*)g, p, lits + C.lit_out + start, cap, &count,
+      st = huf_stream(blk + off, C.stream_size[k], lo, (g_u16*)g, p, lits + C.lit_out + start, cap, &count,
                               slack);
     counts[b][k] = count;
     errs[b][k] = st;
@@ -1229,11 +1417,14 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
       (void)huf_stream_deep(blk + off, C.stream_size[k], (uintptr_t)src, (const uint32_t*)g, p, lits + C.lit_out + at,
                             counts[b][k], &count);
     else if (use_lds)
-      (void)huf_stream<const lds_u16*>(blk + off, C.stream_size[k], (uintptr_t)src,
-                                       (const lds_u16*)lut[b], p, lits + C.lit_out + at, counts[b][k], &count,
-                                       lits + C.lit_out + R + 16 + C.lit_extra);
+      (void)huf_stream_pr<const lds_u32*>(blk + off, C.stream_size[k], (uintptr_t)src, (const lds_u32*)dl[b], L, p,
+                                          lits + C.lit_out + at, counts[b][k], &count,
+                                          lits + C.lit_out + R + 16 + C.lit_extra);
+    else if (p <= K2_LUT_BITS)
+      (void)huf_stream_pr<gc_u32*>(blk + off, C.stream_size[k], (uintptr_t)src, (gc_u32*)g, L, p, lits + C.lit_out + at,
+                                  counts[b][k], &count, lits + C.lit_out + R + 16 + C.lit_extra);
     else
-      (void)huf_stream<g_u16*>(blk + off, C.stream_size[k], (uintptr_t)src, (g_u16*)g, p,
+      (void)huf_stream(blk + off, C.stream_size[k], (uintptr_t)src, (g_u16*)g, p,
                                lits + C.lit_out + at, counts[b][k], &count, lits + C.lit_out + R + 16 + C.lit_extra);
   }
   // zd_k_fused's K4 waves wait for every K2 workgroup: the workgroup (one
@@ -4112,9 +4303,13 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        huge);
     hipLaunchKernelGGL(pass_big, g, b, 0, st, a.src, a.src_size, comp, cstate, fstate, lt, a.n_tables, luts, fses,
                        huge);
-    if (huf)                                   // the trees of more than 256 symbols the two passes listed
+    if (huf) {                                 // the trees of more than 256 symbols the two passes listed
       hipLaunchKernelGGL(zd_k_tables_huge, dim3(K1H_GRID), dim3(K1H_LANES), 0, st, a.src, a.src_size, comp, cstate,
                          fstate, (const uint32_t*)huge, luts);
+      // K2's pair tables, from the LUTs of maxBits <= 11
+      hipLaunchKernelGGL(zd_k_huf_pairs, dim3((a.n_tables + PR_WAVES - 1) / PR_WAVES), dim3(64 * PR_WAVES), 0, st,
+                         comp, (const CompState*)cstate, lt, a.n_tables, luts);
+    }
   };
   const bool fz = a.fused && !a.events;
   auto k1seqw = [&](hipStream_t st) {

@@ -155,7 +155,7 @@ ZD_HD void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hb
           if (most > cb.lit_regen) cb.lit_extra = (uint32_t)(most - cb.lit_regen);
         }
         cb.lit_out = c.lits;
-        c.lits += plan_align((uint64_t)cb.lit_regen + 24 + cb.lit_extra, X.fused ? 128 : 16);   // + K2's 8-byte slack
+        c.lits += plan_align((uint64_t)cb.lit_regen + 32 + cb.lit_extra, X.fused ? 128 : 16);   // + K2's 16-byte slack
       }
       if (X.fused) c.nrec = plan_align(c.nrec, 16);   // a block's records start a 128-byte line
       cb.seq_out = c.nrec;
