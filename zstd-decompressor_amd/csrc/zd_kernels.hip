@@ -1899,13 +1899,21 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     s = (ns << nb) + v - Tr;   // (the next address formed from v in one op: 2.07 -> 2.11 ms on C3)
   };
   uint32_t i = 0;
+  // a trip runs while i + 1 < n, so with U = 4 its pairs i, i + 2 are <= n,
+  // and a pair at n (n even) is the spare pair: the pair stores walk a pointer
+  g_u32* wp = outw;
   for (; i + 1 < n; i += U) {
 #pragma unroll
     for (int k = 0; k < U; k += 2) {
       step(w[k % L]);
       asm volatile("" ::: "memory");
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
-      outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
+      if constexpr (U == 4) {
+        *wp = pair_word(s, (uint32_t)pos);
+        wp += 4;
+      } else {
+        outw[2 * (slot < n ? slot : n_even)] = pair_word(s, (uint32_t)pos);
+      }
       if constexpr (PUB) {
         // The line published here ends with pair slot - 14, seven pairs back;
         // each pair since issued K3_PAIR_VMEM vector-memory ops (two window
