@@ -1116,16 +1116,27 @@ __device__ int huf_stream_pr(const uint8_t* bs, uint32_t size, uintptr_t base, T
   auto group = [&](Win6& w) {
     uint64_t acc[2];
     uint32_t n[2], used = 0, bad = 0;
+    // the group's 96 bits below pos, MSB first in (hi, lo, x), taken from the
+    // window once: sp = pos - wb - 96 in 0..96 (the window covers >= 97 bits
+    // below pos; bits under it read as 0 and a group consumes <= 88)
+    const uint32_t sp = (uint32_t)(pos - w.wb - 96);
+    const bool b0 = (sp & 32) != 0, b1 = (sp & 64) != 0;
+    const uint32_t a0 = b0 ? w.w1 : w.w0, a1 = b0 ? w.w2 : w.w1, a2 = b0 ? w.w3 : w.w2;
+    const uint32_t a3 = b0 ? w.w4 : w.w3, a4 = b0 ? w.w5 : w.w4, a5 = b0 ? 0u : w.w5;
+    const uint32_t c0 = b1 ? a2 : a0, c1 = b1 ? a3 : a1, c2 = b1 ? a4 : a2, c3 = b1 ? a5 : a3;
+    uint32_t hi = __builtin_amdgcn_alignbit(c3, c2, sp), lo = __builtin_amdgcn_alignbit(c2, c1, sp);
+    uint32_t x = __builtin_amdgcn_alignbit(c1, c0, sp);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      const uint64_t t = win6_top64(w, pos - (int32_t)used);
-      uint32_t hi = (uint32_t)(t >> 32), lo = (uint32_t)t, S = 0;
+      // half 1 peeks at most 3 * 11 + 11 bits past its start: hi:lo hold them
+      uint32_t S = 0;
       uint64_t a = 0;
 #pragma unroll
       for (int j = 0; j < K2_GROUP / 2; j++) {
         const uint32_t e = dl[pr_index(hi >> 21, L)];
         hi = __builtin_amdgcn_alignbit(hi, lo, e);
-        lo = __builtin_amdgcn_alignbit(lo, 0u, e);
+        lo = __builtin_amdgcn_alignbit(lo, h == 0 ? x : 0u, e);
+        if (h == 0) x = __builtin_amdgcn_alignbit(x, 0u, e);
         const uint32_t c8 = 8 * j + 8 * ((S >> 8) & 7);          // bytes before this lookup's
         a |= (uint64_t)(e >> 16) << c8;
         S += e;
