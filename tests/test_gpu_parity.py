@@ -589,6 +589,115 @@ def test_k2_trees_deeper_than_the_lut():
     assert ost == 0
 
 
+def _pair_table_kind(weights):
+    """Which pair-table entries a tree of direct weights gives K2
+    (zd_kernels.hip PR_*): None when the reference panics building it, else
+    (p, L, long) -- maxBits, the leading 10-bit prefixes split into 11-bit
+    halves, and whether a deep prefix lies past them (PR_LONG).  Restates
+    from_weights + insert (huffman.rs:132-203) as K1 places the codes:
+    longest first, each width from the next aligned slot; gaps are absent
+    nodes."""
+    ws = [w for w in weights if w]
+    if not ws or max(ws) > 32:
+        return None
+    total = sum(1 << (w - 1) for w in ws)
+    p = total.bit_length() - 1
+    if (1 << p) < total:
+        p += 1
+    rest = (1 << p) - total
+    if rest == 0 or rest > 255 or max(ws) > p + 1:
+        return None
+    manq = rest.bit_length()
+    if manq > p + 1 or p > 11:
+        return None
+    cnt = {}
+    for w in list(ws) + [manq]:
+        cnt[p + 1 - w] = cnt.get(p + 1 - w, 0) + 1
+    T, pos, width = 1 << p, 0, [0] * (1 << p)
+    holes = []
+    for w in range(p, 0, -1):
+        if not cnt.get(w):
+            continue
+        S = 1 << (p - w)
+        al = (pos + S - 1) & ~(S - 1)
+        holes.append((pos, al))
+        k = min(cnt[w], (T - al) // S)
+        for e in range(al, al + k * S):
+            width[e] = w
+        pos = al + k * S
+    holes.append((pos, T))
+    for a, b in holes:
+        for e in range(a, b):
+            k = p
+            while k > 0 and not ((e & ~((1 << k) - 1)) >= a and (e & ~((1 << k) - 1)) + (1 << k) <= b):
+                k -= 1
+            width[e] = p - k
+    if p < 11:
+        return p, 0, False
+    deep = [width[2 * i] > 10 or width[2 * i + 1] > 10 for i in range(1024)]
+    L = next((i for i, d in enumerate(deep) if not d), 1024)
+    return p, min(L, 128), any(deep[i] for i in range(min(L, 128), 1024))
+
+
+def test_k2_pair_tables():
+    """K2's pair tables (zd_k_huf_pairs, huf_stream_pr): trees of maxBits
+    1..11 with no 11-bit codes (no split prefixes) and with split leading
+    prefixes, complete (frames the reference decodes, so the literal bytes
+    are compared) and incomplete (absent nodes: the reference panics or runs
+    out of bits), over streams of 12 bytes (the exact path alone) to 400 (the
+    fast loop), each frame against the oracle, alone and beside libzstd
+    frames.  (Deep prefixes past the leading run -- PR_LONG -- need more than
+    256 leaves, K1's huge-tree pass: a tree description of direct weights
+    cannot reach them, and _pair_table_kind never reports one here.)"""
+    r = random.Random(31)
+    want = {("short", True): 6, ("split", True): 6, ("short", False): 4, ("split", False): 4}
+    got = {k: [] for k in want}
+    for _ in range(40000):
+        if all(len(got[k]) >= want[k] for k in want):
+            break
+        if r.random() < 0.5:
+            n = r.randrange(2, 128)
+            top = r.choice([4, 8, 11, 12])
+            weights = [r.choice([0, r.randrange(1, top)]) for _ in range(n)]
+        else:                                             # a complete code with 11-bit codes: split leaves
+            lens = [0]
+            while len(lens) < r.randrange(8, 120) or max(lens) < 11:
+                cand = [i for i, l in enumerate(lens) if l < 11]
+                i = r.choice(cand) if r.random() < 0.6 else max(cand, key=lambda c: lens[c])
+                lens[i] += 1
+                lens.append(lens[i])
+            r.shuffle(lens)
+            weights = [12 - l for l in lens[:-1]]         # the last symbol is the implied one
+        kind = _pair_table_kind(weights)
+        if kind is None:
+            continue
+        p, L, lng = kind
+        assert not lng
+        total = sum(1 << (w - 1) for w in weights if w)
+        rest = (1 << p) - total
+        complete = rest & (rest - 1) == 0                 # the implied symbol fills the tree
+        k = ("split" if L else "short", complete)
+        if len(got[k]) >= want[k]:
+            continue
+        f = _deep_tree_frame(r, 400, weights)
+        if complete and oracle.decompress_status(f, False)[0] != 0:
+            continue                                      # (the random sequence failed)
+        got[k].append((weights, f))
+    assert all(len(got[k]) >= want[k] for k in want), {k: len(v) for k, v in got.items()}
+    frames = []
+    for k in want:
+        for weights, f in got[k]:
+            frames += [f, _deep_tree_frame(r, 12, weights), _deep_tree_frame(r, 60, weights)]
+    for i, f in enumerate(frames):
+        assert_parity(f, False, f"pair table #{i}")
+    src = gen.text(200_000, seed=6)
+    parts = []
+    for i, f in enumerate(frames[::3]):
+        parts.append(f)
+        parts.append(gen.frames(src[i * 5_000:(i + 1) * 5_000], 5_000, 3))
+    assert_parity(b"".join(parts), False, "pair tables beside libzstd frames")
+
+
 @pytest.mark.parametrize("shape", ["one_frame", "forked_300_frames", "block_parallel"])
 def test_hip_graph_capture_replay(shape):
     """zd_decode_async is graph-safe (include/zd.h): no allocation, no host
