@@ -3641,10 +3641,13 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 // order on one wave: a 100 MB frame (the stock `zstd enwik8` shape) is ~11 M
 // sequences one batch after another.  K4J takes the frame's serial
 // dependencies apart:
-//   KJ1 zd_k_jsum     one wave per block: the block's output size (literals +
-//                     match lengths) and its repeat-offset map (decode_offset
-//                     as a function of the three offsets coming in, jr codes),
-//                     with a checkpoint every J_SEG sequences (JSeg)
+//   KJ1 zd_k_jsum     one wave per J_SEG sequences of a block: the segment's
+//                     output and literal bytes and its repeat-offset map
+//                     (decode_offset as a function of the three offsets coming
+//                     in, jr codes); then zd_k_jsum_blocks, one lane per block,
+//                     turns its segments' sums into checkpoints (JSeg: the
+//                     bytes and map before each segment) and gives the block's
+//                     output size (literals + match lengths) and map
 //   KJ2 zd_k_jprefix  one wave per frame: scans over the blocks give each
 //                     block's output position and the concrete repeat offsets
 //                     entering it; the capacity check
@@ -3824,22 +3827,67 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
                                                 const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp,
                                                 const CompState* __restrict__ cstate, const uint64_t* __restrict__ seqs,
                                                 const uint16_t* __restrict__ fses, const JFrame* __restrict__ jframes,
-                                                const JBlkDesc* __restrict__ jd, JBlk* __restrict__ jb,
+                                                const JBlkDesc* __restrict__ jd, const JSegDesc* __restrict__ jsd,
                                                 JSeg* __restrict__ jseg) {
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
   const int lane = threadIdx.x;
-  const uint32_t e = blockIdx.x;
+  const JSegDesc SD = jsd[blockIdx.x];
+  const JBlkDesc D = jd[SD.jblk];
+  const uint64_t key0 = fstate[jframes[D.jframe].frame].key;
+  const BlockRec B = blocks[D.block];
+  // the segment's sums, written in place of its checkpoint (zd_k_jsum_blocks)
+  uint64_t rep[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
+  uint64_t out = 0;                                 // uniform
+  uint32_t lit = 0;
+  if (j_live(key0, D.j) && B.type == 2) {
+    const CompState CS = cstate[B.comp];
+    const CompBlock C = comp[B.comp];
+    const uint32_t n = C.nseq, sb = SD.k * J_SEG, se = min(n, sb + J_SEG);
+    if (!CS.stop && se > sb) {
+      j_stab(stab, C, comp, cstate, fses, lane);
+      JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, se, C.seq_direct != 0};
+      R.start(sb, lane);
+      for (uint32_t s0 = sb; s0 < se; s0 += 64) {
+        const int k = (int)min(64u, se - s0);
+        uint32_t ll = 0, ml = 0, ofv = 4;
+        if (lane < k) j_values(R.recA, R.winA, stab, ll, ml, ofv);
+        R.next(s0, lane);
+        int bl, bc;
+        (void)j_offsets<true>(ofv, ll, k, rep, &bl, &bc);
+        const uint32_t it = wave_scan_incl(ll + ml), il = wave_scan_incl(ll);
+        out += (uint32_t)__builtin_amdgcn_readlane((int)it, 63);
+        lit += (uint32_t)__builtin_amdgcn_readlane((int)il, 63);
+      }
+    }
+  }
+  if (lane == 0) {
+    JSeg g{};
+    g.out_rel = out;
+    g.lit_rel = lit;
+    g.map[0] = rep[0]; g.map[1] = rep[1]; g.map[2] = rep[2];
+    jseg[D.seg0 + SD.k] = g;
+  }
+}
+
+// KJ1, second part: one lane per block.  Its segments' sums become the
+// checkpoints KJ3 starts from (bytes before the segment, the map before it as
+// jr codes of the block's incoming offsets: the maps compose with jr_apply);
+// the block's output size is its literals plus its match lengths.
+__global__ __launch_bounds__(64) void zd_k_jsum_blocks(const FrameState* __restrict__ fstate,
+                                                       const BlockRec* __restrict__ blocks,
+                                                       const CompBlock* __restrict__ comp,
+                                                       const CompState* __restrict__ cstate,
+                                                       const JFrame* __restrict__ jframes,
+                                                       const JBlkDesc* __restrict__ jd, uint32_t n_jblk,
+                                                       JBlk* __restrict__ jb, JSeg* __restrict__ jseg) {
+  const uint32_t e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= n_jblk) return;
   const JBlkDesc D = jd[e];
   const uint64_t key0 = fstate[jframes[D.jframe].frame].key;
   const BlockRec B = blocks[D.block];
-  uint64_t rep[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
+  uint64_t map[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
   uint64_t size = 0;
   uint32_t dead = j_live(key0, D.j) ? 0u : 1u;
-  if (lane == 0) {                                  // segment 0 starts the block
-    JSeg g{};
-    g.map[0] = rep[0]; g.map[1] = rep[1]; g.map[2] = rep[2];
-    jseg[D.seg0] = g;
-  }
   if (!dead && B.type != 2) {
     size = B.size;                                  // raw / RLE (block.rs:76-79)
   } else if (!dead) {
@@ -3849,42 +3897,28 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
       dead = 1;
     } else {
       const uint32_t nl = (C.lit_type == LIT_RAW || C.lit_type == LIT_RLE) ? C.lit_regen : CS.lit_count;
-      uint64_t out_rel = 0;                         // uniform
-      uint32_t lit_rel = 0;
-      const uint32_t n = C.nseq;
-      if (n) {
-        j_stab(stab, C, comp, cstate, fses, lane);
-        JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, n, C.seq_direct != 0};
-        R.start(0, lane);
-        for (uint32_t s0 = 0; s0 < n; s0 += 64) {
-          if (s0 && s0 % J_SEG == 0 && lane == 0) {  // a checkpoint for KJ3's segment
-            JSeg g{};
-            g.out_rel = out_rel;
-            g.map[0] = rep[0]; g.map[1] = rep[1]; g.map[2] = rep[2];
-            g.lit_rel = lit_rel;
-            jseg[D.seg0 + s0 / J_SEG] = g;
-          }
-          const int k = (int)min(64u, n - s0);
-          uint32_t ll = 0, ml = 0, ofv = 4;
-          if (lane < k) j_values(R.recA, R.winA, stab, ll, ml, ofv);
-          R.next(s0, lane);
-          int bl, bc;
-          (void)j_offsets<true>(ofv, ll, k, rep, &bl, &bc);
-          const uint32_t it = wave_scan_incl(ll + ml), il = wave_scan_incl(ll);
-          out_rel += (uint32_t)__builtin_amdgcn_readlane((int)it, 63);
-          lit_rel += (uint32_t)__builtin_amdgcn_readlane((int)il, 63);
-        }
+      const uint32_t nseg = C.nseq > J_SEG ? (C.nseq + J_SEG - 1) / J_SEG : 1;
+      uint64_t out = 0;
+      uint32_t lit = 0;
+      for (uint32_t k = 0; k < nseg; k++) {
+        JSeg& g = jseg[D.seg0 + k];
+        const JSeg t = g;                           // the segment's own sums
+        g.out_rel = out;
+        g.lit_rel = lit;
+        g.map[0] = map[0]; g.map[1] = map[1]; g.map[2] = map[2];
+        out += t.out_rel;
+        lit += t.lit_rel;
+        const uint64_t m0 = jr_apply(t.map[0], map), m1 = jr_apply(t.map[1], map), m2 = jr_apply(t.map[2], map);
+        map[0] = m0; map[1] = m1; map[2] = m2;
       }
-      size = (uint64_t)nl + out_rel - lit_rel;      // literals + match lengths
+      size = (uint64_t)nl + out - lit;              // literals + match lengths
     }
   }
-  if (lane == 0) {
-    jb[e].size = size;
-    jb[e].map[0] = rep[0];
-    jb[e].map[1] = rep[1];
-    jb[e].map[2] = rep[2];
-    jb[e].dead = dead;
-  }
+  jb[e].size = size;
+  jb[e].map[0] = map[0];
+  jb[e].map[1] = map[1];
+  jb[e].map[2] = map[2];
+  jb[e].dead = dead;
 }
 
 __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__ frames, FrameState* fstate,
@@ -4417,8 +4451,10 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     auto* jsd = (const JSegDesc*)(ws + W.jsegd);
     auto* jst = (uint32_t*)(ws + W.jst);
     auto* pend = (uint32_t*)(ws + W.jpend);
-    hipLaunchKernelGGL(zd_k_jsum, dim3(a.n_jblk), dim3(64), 0, s, a.src, (const FrameState*)fstate, blocks, comp,
-                       (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jb, jseg);
+    hipLaunchKernelGGL(zd_k_jsum, dim3(a.n_jseg), dim3(64), 0, s, a.src, (const FrameState*)fstate, blocks, comp,
+                       (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jsd, jseg);
+    hipLaunchKernelGGL(zd_k_jsum_blocks, dim3((a.n_jblk + 63) / 64), dim3(64), 0, s, (const FrameState*)fstate,
+                       blocks, comp, (const CompState*)cstate, jframes, jd, a.n_jblk, jb, jseg);
     hipLaunchKernelGGL(zd_k_jprefix, dim3(a.n_jframes), dim3(64), 0, s, frames, fstate, jframes, jd, jb);
     hipLaunchKernelGGL(zd_k_jscatter, dim3(a.n_jseg), dim3(64), 0, s, a.src, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
