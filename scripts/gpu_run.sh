@@ -44,6 +44,7 @@ for s in "$@"; do
     pmck2) run pmc_k2a 300 rocprofv3 --kernel-trace --kernel-include-regex "zd_k_huffman|zd_k_huf_pairs" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc_k2a -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io && run pmc_k2b 300 rocprofv3 --kernel-trace --kernel-include-regex "zd_k_huffman" --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM -d gpurun_out/pmc_k2b -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io ;;
     varx:*) v=${s#varx:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run bench_varx_$v 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io --no-verify --experiment ;;
     prof10) run prof10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10 -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
+    pmc10) run pmc_sq10 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY -d gpurun_out/pmc_sq10 -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io ;;
     pmchbm10) run pmc_fetch10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch10 -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io && run pmc_write10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write10 -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io ;;
     benchc5:*) l=${s#benchc5:}; run bench_c5_L$l 900 python bench.py --workload c5 --level $l --no-host-io ;;
     benchc2) run bench_c2 600 python bench.py --workload c2 ;;
