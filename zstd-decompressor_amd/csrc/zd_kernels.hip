@@ -1,17 +1,20 @@
-// zd_kernels.hip — gfx950 kernels of the ZSTD block-decode path.
+// zd_kernels.hip — gfx950 kernels of the ZSTD block-decode path (DESIGN.md §4).
 //
-//   K1 zd_k_tables     one wave per compressed block: Huffman tree description
+//   K0 zd_k_rawcopy    raw / RLE blocks that lead a frame (block.rs:76-79)
+//   K1 zd_k_tables     one compressed block per lane: Huffman tree description
 //                      -> LUT, FSE table descriptions -> decode tables
-//                      (replaces huffman.rs:80-203, fse.rs:16-202,
-//                      sequences.rs:91-187 table construction)
-//   K2 zd_k_huffman    one wave per Huffman-literal block, LUT in LDS, one lane
-//                      per stream (replaces literals.rs:49-86 + huffman.rs:205-218)
-//   K3 zd_k_sequences  one wave per block, tables in LDS, FSE state machine
-//                      (replaces sequences.rs:191-237 + decoders/sequence.rs)
-//   K4 zd_k_execute    one wave per frame, 8 KiB LDS window ring, 64 sequences
-//                      per step: repeat-offset transforms by wave scan, literal
-//                      and match copies into the ring, aligned 16-B flushes to
-//                      HBM (replaces decoding_context.rs:50-106 + block.rs:74-99)
+//                      (huffman.rs:80-203, fse.rs:16-202, sequences.rs:91-187);
+//                      zd_k_tables_seqw: the sequence tables one wave per block;
+//                      zd_k_huf_pairs: each LUT of <= 11 bits -> K2's pair table
+//   K2 zd_k_huffman    one stream per lane, 8 blocks per wave, pair tables in
+//                      LDS (literals.rs:49-86 + huffman.rs:205-218)
+//   K3 zd_k_sequences_q  the FSE state chain, four lanes per block, 16 blocks
+//                      per wave, tables in LDS (sequences.rs:191-237)
+//   K4 zd_k_execute    one wave per frame, 64 sequences per batch, a linear LDS
+//                      window of recent output, aligned 16-B flushes to HBM
+//                      (decoding_context.rs:50-106 + block.rs:74-99, with the
+//                      value decode of decoders/sequence.rs:41-55); K4F / K4J /
+//                      zd_k_fused: the executors for other plan shapes
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
