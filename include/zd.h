@@ -268,9 +268,12 @@ int zd_plan_checksums(zd_plan* plan, const uint8_t* d_dst, void* stream, int32_t
 /* Kernel times of the last zd_decode_async on the plan, in ms (HIP events on
  * the plan's stream).  zd_plan_set_profiling mode 1: every kernel timed, the
  * launches one after another (no K2 | K3 fork, no fused kernel); mode 2: the
- * pipeline exactly as it runs unprofiled, with events around its dominant
- * launch only (one entry: "zd_k_fused" in fused plans, else "zd_k_execute");
- * 0: off.  names/ms arrays of cap entries. */
+ * pipeline exactly as it runs unprofiled, with events around each launch
+ * group that can carry the plan's work and did launch, one entry each, in
+ * this order: "zd_k_rawcopy" (K0, raw/RLE blocks), "zd_k_fused", "zd_k_execute"
+ * (only when some frame runs on it), "zd_k_execute_lds" (K4F), and the K4J
+ * kernels together ("zd_k_jsum+...+zd_k_jround"); the largest is the
+ * dominant launch.  0: off.  names/ms arrays of cap entries. */
 int zd_plan_set_profiling(zd_plan* plan, int enable);
 int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, int* n);
 
@@ -282,9 +285,11 @@ int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, 
  * it (its Frame_Content_Size, or 128 KiB per block) is planned again from its
  * own start with more room, as often as needed (info.replans); the reference
  * checks neither (decoding_context.rs:29-47, block.rs:50).  Calls on distinct
- * plans may run on distinct threads: they share one process-wide pair of
- * pinned chunks only while copying (the copies serialise, the decodes
- * overlap); one plan is not used from two threads at once. */
+ * plans may run on distinct threads (thread safe: they share one
+ * process-wide pair of pinned chunks only while copying).  Every call runs on
+ * the device's legacy null stream, so concurrent calls do not overlap on the
+ * GPU; a caller that wants overlap uses zd_decode_async on its own streams.
+ * One plan is not used from two threads at once. */
 int zd_plan_decompress(zd_plan* plan, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 /* Convenience: host in, host out (H2D + decode + D2H on the default
  * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
@@ -322,6 +327,11 @@ typedef struct zd_comm zd_comm;
 int zd_comm_unique_id(uint8_t id[ZD_COMM_ID_BYTES]);
 int zd_comm_create(const uint8_t id[ZD_COMM_ID_BYTES], int world, int rank, zd_comm** out);
 void zd_comm_destroy(zd_comm* comm);
+/* The device buffers zd_decode_sharded keeps in the communicator between
+ * calls (its input copy and its own output buffer), in bytes: memory
+ * accounting.  A rank-0 decode that outgrows the caller's d_root_out moves to
+ * an output buffer sized from what it needs, never from root_cap. */
+int zd_comm_buffers(const zd_comm* comm, uint64_t* src_bytes, uint64_t* out_bytes);
 
 typedef struct zd_gather_result {
   uint64_t total_len;         /* bytes gathered on rank 0 */

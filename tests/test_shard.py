@@ -240,6 +240,33 @@ def _comm_world1_worker(port, q):
                 if st3 != 0 or res3.status != ost or got != oout:
                     bad.append((name, st3, res3.status, ost, res3.total_len, len(oout)))
         comm.close()
+        # a rank-0 re-plan that outgrows the lent root buffer: the comm's own
+        # output buffer is sized from what the re-plan needs, not from root_cap
+        # (a fresh comm, so no earlier buffer is reused)
+        from zstd_decompressor.batch import Plan
+        data, need = _late_overrun_case()
+        ost, oout = oracle.decompress_status(data, False)
+        pl = Plan(data)
+        root_cap = int(pl.info.out_bytes) + 64
+        pl.close()
+        assert need > root_cap and len(oout) <= need
+        comm = shard.Comm(0, 1, dev)
+        out = torch.zeros(len(oout) + 64, dtype=torch.uint8, device=dev)
+        res4 = _lib.GatherResult()
+        p, n, keep = _lib.buf(data)
+        st4 = _lib.lib().zd_decode_sharded(comm._h, p, n, 0, C.c_void_p(out.data_ptr()), root_cap, C.byref(res4),
+                                           C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        torch.cuda.synchronize(dev)
+        sb, ob = C.c_uint64(), C.c_uint64()
+        _lib.check(_lib.lib().zd_comm_buffers(comm._h, C.byref(sb), C.byref(ob)), "zd_comm_buffers")
+        # the output itself comes back through the gather into `out`: root_cap
+        # is short of it, so the call reports DST_TOO_SMALL or decodes in full
+        if not (st4 == _lib.DST_TOO_SMALL or res4.status == _lib.DST_TOO_SMALL or
+                (st4 == 0 and bytes(out[:res4.total_len].cpu().numpy().tobytes()) == oout)):
+            bad.append(("late overrun", st4, res4.status))
+        if not (need <= ob.value < root_cap + root_cap // 2):
+            bad.append(("late overrun buffer", ob.value, need, root_cap))
+        comm.close()
         q.put((ok1, ok2, bad))
     finally:
         dist.destroy_process_group()
@@ -297,6 +324,18 @@ def _sharded_cases():
         ("deep tree", fr[0] + deep + fr[1] + deep + fr[2]),
         ("corrupt middle", b"".join(fr[:3]) + bytes(corrupt) + b"".join(fr[4:])),
     ]
+
+
+def _late_overrun_case():
+    """40 frames of 100,000 bytes, frame 38 claiming an FCS of 3000: the plan
+    reserves 3,903,000 bytes, the re-plan from frame 38 on needs the 3,800,000
+    before it plus 3000 + 1 MiB for it (zd_host.cpp decode_resident) plus
+    frame 39's 100,000.  Returns (input, bytes the re-plan needs)."""
+    from corpus import gen
+    src = gen.text(4_000_000, seed=29)
+    fr = [gen.frames(src[i * 100_000:(i + 1) * 100_000], 100_000, 3) for i in range(40)]
+    need = 38 * 100_000 + 3000 + (1 << 20) + 100_000
+    return b"".join(fr[:38]) + _lower_fcs(fr[38], 3000) + fr[39], need
 
 
 def oracle_status(data: bytes) -> int:

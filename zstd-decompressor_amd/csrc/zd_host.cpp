@@ -98,16 +98,22 @@ struct zd_plan {
   // frame index stays in the workspace (W.hframes) until a caller needs it
   bool dev_built = false;
   mutable std::vector<HostFrame> dev_frames;
-  const HostFrame& frame(size_t f) const {
-    if (dev_built) {
-      if (dev_frames.size() != nframes) {
-        dev_frames.resize(nframes);
-        if (nframes && hipMemcpy(dev_frames.data(), d_ws + W.hframes, nframes * sizeof(HostFrame),
-                                 hipMemcpyDeviceToHost) != hipSuccess)
-          (void)hipGetLastError();
-      }
-      return dev_frames[f];
+  // the frame index on the host (a device-built plan's comes back once);
+  // false when it cannot be read -- nothing is kept then, a later call retries
+  bool frames_ready() const {
+    if (!dev_built || dev_frames.size() == nframes) return true;
+    std::vector<HostFrame> v(nframes);
+    if (nframes && hipMemcpy(v.data(), d_ws + W.hframes, nframes * sizeof(HostFrame), hipMemcpyDeviceToHost) !=
+                       hipSuccess) {
+      (void)hipGetLastError();
+      return false;
     }
+    dev_frames = std::move(v);
+    return true;
+  }
+  // (callers check frames_ready() first)
+  const HostFrame& frame(size_t f) const {
+    if (dev_built) return dev_frames[f];
     const size_t k = (size_t)(std::upper_bound(part_f0.begin(), part_f0.end(), f) - part_f0.begin()) - 1;
     return parts[k].frames[f - part_f0[k]];
   }
@@ -118,9 +124,9 @@ struct zd_plan {
     for (const HostPart& hp : parts) { part_f0.push_back(nframes); nframes += hp.frames.size(); }
   }
   bool profile = false;                  // mode 1: every kernel timed, one after another
-  bool profile_dom = false;              // mode 2: the dominant launch timed in the pipeline as it runs
-  bool dom_fused = false;                // the last mode-2 launch timed zd_k_fused (else zd_k_execute)
-  hipEvent_t dom_ev[2] = {};
+  bool profile_dom = false;              // mode 2: the launch groups that carry work, timed in the pipeline as it runs
+  uint32_t dom_used = 0;                 // the groups (kDomNames) the last mode-2 launch recorded
+  hipEvent_t dom_ev[2 * N_DOM] = {};
   hipEvent_t ev[N_KERNELS + 1] = {};
   bool ev_made = false;
   bool launched = false;
@@ -1564,14 +1570,17 @@ int zd_plan_set_profiling(zd_plan* P, int enable) {
 int zd_plan_kernel_times(zd_plan* P, const char** names, float* ms, int cap, int* n) {
   if (!P || !P->launched || !(P->profile || P->profile_dom)) return ZD_E_INVALID_ARG;
   if (P->profile_dom) {
-    HIPCHK(hipEventSynchronize(P->dom_ev[1]));
-    float t = 0;
-    HIPCHK(hipEventElapsedTime(&t, P->dom_ev[0], P->dom_ev[1]));
-    if (cap > 0) {
-      if (names) names[0] = P->dom_fused ? "zd_k_fused" : "zd_k_execute";
-      if (ms) ms[0] = t;
+    int k = 0;
+    for (int g = 0; g < N_DOM && k < cap; g++) {
+      if (!(P->dom_used >> g & 1)) continue;
+      HIPCHK(hipEventSynchronize(P->dom_ev[2 * g + 1]));
+      float t = 0;
+      HIPCHK(hipEventElapsedTime(&t, P->dom_ev[2 * g], P->dom_ev[2 * g + 1]));
+      if (names) names[k] = kDomNames[g];
+      if (ms) ms[k] = t;
+      k++;
     }
-    if (n) *n = cap > 0 ? 1 : 0;
+    if (n) *n = k;
     return ZD_OK;
   }
   HIPCHK(hipEventSynchronize(P->ev[N_KERNELS]));
@@ -1656,7 +1665,8 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   }
   if (P->profile_dom) {
     a.dom_events = P->dom_ev;
-    P->dom_fused = a.fused;
+    P->dom_used = 0;
+    a.dom_used = &P->dom_used;
   }
   HIPCHK(launch_pipeline(a));
   P->launched = true;
@@ -1762,6 +1772,7 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
     if (e == hipSuccess) e = hipMemcpy(h.data(), d + 2 * m, m * 8, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return ZD_E_HIP;
   }
+  if (!P->frames_ready()) return ZD_E_HIP;
   for (size_t f = 0; f < nf; f++) {
     const zd_frame_desc& d = P->frame(f).d;
     const bool have = f < m && d.kind == ZD_FRAME_ZSTD && d.has_checksum;
@@ -1775,12 +1786,24 @@ int zd_plan_checksums(zd_plan* P, const uint8_t* d_dst, void* stream, int32_t* o
 
 namespace {
 
-// Makes o hold `need` bytes, keeping its first `keep` (a new allocation in
-// the caller's *o.own when o is short; o.p itself is freed only when it is
-// that allocation).
+// Makes o hold `need` bytes, keeping its first `keep`.  When o.p is the
+// caller's own allocation (*o.own) it grows by half at least; when o.p is a
+// buffer the caller lent (rank 0's gather buffer in zd_decode_sharded) the
+// kept allocation *o.own is reused if it holds `need`, else replaced by one of
+// `need` bytes (half again over its old size at most) -- never sized from the
+// lent buffer.
 int devout_reserve(DevOut& o, uint64_t need, uint64_t keep, hipStream_t s) {
   if (need <= o.cap) return 0;
-  const uint64_t want = std::max<uint64_t>(need, o.cap + o.cap / 2);
+  const bool lent = o.p != *o.own;
+  if (lent && *o.own && *o.own_cap >= need) {
+    if (keep) HIPCHK(hipMemcpyAsync(*o.own, o.p, keep, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    o.p = *o.own;
+    o.cap = *o.own_cap;
+    return 0;
+  }
+  const uint64_t base = lent ? (*o.own ? *o.own_cap : 0) : o.cap;
+  const uint64_t want = std::max<uint64_t>(need, base + base / 2);
   uint8_t* q = nullptr;
   if (hipMalloc(&q, want) != hipSuccess) {
     (void)hipGetLastError();
@@ -1839,6 +1862,7 @@ int zd::decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t*
       flags = (flags & ~ZD_F_BLOCK_PARALLEL) | ZD_F_FRAME_SERIAL;
       cap0 = old_cap;
     }
+    if (!cur->frames_ready()) { st = ZD_E_HIP; break; }
     const size_t at = base + (size_t)cur->frame(f).d.src_offset;
     zd_plan* Q = nullptr;
     const int r = plan_create(src + at, nullptr, n - at, flags, nullptr, &Q, cap0);

@@ -28,6 +28,8 @@ namespace zd {
 
 const char* const kKernelNames[N_KERNELS] = {"zd_k_rawcopy", "zd_k_tables", "zd_k_huffman", "zd_k_sequences",
                                              "zd_k_execute", "zd_k_jexec"};
+const char* const kDomNames[N_DOM] = {"zd_k_rawcopy", "zd_k_fused", "zd_k_execute", "zd_k_execute_lds",
+                                      "zd_k_jsum+zd_k_jsum_blocks+zd_k_jprefix+zd_k_jscatter+zd_k_jround"};
 
 // ---------------------------------------------------------------------------
 // constants (decoders/sequence.rs:95-191, sequences.rs:29-39)
@@ -1158,11 +1160,7 @@ __device__ int huf_stream_pr(const uint8_t* bs, uint32_t size, uintptr_t base, T
     const uint32_t s0 = 8 * n[0] - 32;                      // 0..32
     const uint64_t v0 = acc[0] | ((acc[1] << s0) << 32);
     const uint64_t v1 = s0 == 32 ? acc[1] : acc[1] >> (32 - s0);
-#ifdef ZD_EXP_K2_NOSTORE                           // experiment: the literals are not stored (wrong output)
-    *(g_u64a1*)dummy = v0 ^ v1;
-#else
     *(gw_u64x2a1*)(ok ? out + count : dummy) = (u64x2a1){v0, v1};
-#endif
     count += ok ? n[0] + n[1] : 0;
     live = ok && pos >= K2_GROUP * LUT_MAX_BITS && count + ROOM <= cap;
   };
@@ -2093,15 +2091,8 @@ __device__ inline u32x4 ldg16(const uint8_t* p) { return *(g_cu32x4a1*)p; }
 // Match sources in HBM are read through the caches: the frame's own recent
 // output, re-read by later matches (plain loads: the nontemporal form took
 // 28.3 ms against 23.4 in round 1)
-#ifdef ZD_EXP_NOFAR
-// timing-only experiment build (wrong output): every match source that
-// would come from HBM comes from the window in LDS instead
-__device__ inline u32x4 ldg16_src(const uint8_t* p) {
-  return *(const l_u32x4a1*)(const l_u8*)(uintptr_t)((uintptr_t)p & 2047);
-}
-#else
+// (timing-only variants that change the output live in tools/exp_variants.patch)
 __device__ inline u32x4 ldg16_src(const uint8_t* p) { return *(g_cu32x4a1*)p; }
-#endif
 // streams read once (records, literals): plain loads (nontemporal loads of
 // the records, windows and literal stage measured slower: 1 GiB K4 2.06 ->
 // 2.11 ms)
@@ -4334,10 +4325,19 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   auto* seqs = (uint64_t*)(ws + W.seqs);
   hipStream_t s = a.stream;
   hipError_t e;
+  // mode 2: events around launch group g on s
+  auto dom = [&](int g, int end) -> hipError_t {
+    if (!a.dom_events) return hipSuccess;
+    if (end) *a.dom_used |= 1u << g;
+    return hipEventRecord(a.dom_events[2 * g + end], s);
+  };
   if (a.events) if ((e = hipEventRecord(a.events[0], s)) != hipSuccess) return e;
-  if (a.n_copies)
+  if (a.n_copies) {
+    if ((e = dom(DOM_K0, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(zd_k_rawcopy, dim3(a.n_copies), dim3(256), 0, s, a.src, a.out,
                        (const CopyDesc*)(ws + W.copies));
+    if ((e = dom(DOM_K0, 1)) != hipSuccess) return e;
+  }
   if (a.events) if ((e = hipEventRecord(a.events[1], s)) != hipSuccess) return e;
   // K2 and K3 are independent once their tables exist: with the fork, K1's
   // Huffman half and K2 run on the aux stream beside K1's sequence half and
@@ -4407,18 +4407,30 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                            cstate, fstate, list, n, (const uint16_t*)fses, seqs);
     }
   };
-  auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st, const uint8_t* redo) {
+  // the streaming K4 runs when some frame is neither K4F's nor K4J's (the
+  // others exit at once in it)
+  const bool k4_work = a.n_frames > a.n_k4f + a.n_jframes;
+  auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st, const uint8_t* redo) -> hipError_t {
     const uint32_t n = f1 - f0;
-    if (n && a.n_frames > a.n_k4f)   // frames on the streaming K4 (K4F's exit at once)
+    if (n && a.n_frames > a.n_k4f) {  // frames on the streaming K4 (K4F's exit at once)
+      const bool tm = !redo && k4_work;
+      if (tm) if ((e = dom(DOM_K4, 0)) != hipSuccess) return e;
       hipLaunchKernelGGL(zd_k_execute, dim3(n),
                          dim3(64), 0, st, a.src, a.out, frames, fstate, blocks, comp, (const CompState*)cstate,
                          (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs, (const uint16_t*)fses, f0, f1, redo);
+      if (tm) if ((e = dom(DOM_K4, 1)) != hipSuccess) return e;
+    }
+    return hipSuccess;
   };
-  auto k4f = [&](const uint32_t* list, uint32_t n, hipStream_t st) {
-    if (n)
+  auto k4f = [&](const uint32_t* list, uint32_t n, hipStream_t st) -> hipError_t {
+    if (n) {
+      if ((e = dom(DOM_K4F, 0)) != hipSuccess) return e;
       hipLaunchKernelGGL(zd_k_execute_lds, dim3(n), dim3(K4F_T), 0, st, a.src, a.out, frames, fstate, blocks, comp,
                          (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                          (const uint16_t*)fses, list);
+      if ((e = dom(DOM_K4F, 1)) != hipSuccess) return e;
+    }
+    return hipSuccess;
   };
   if (fz) {
     // K1's sequence half + K3 + K4 per group of four frames; K2 (forked) signals its workgroups;
@@ -4426,24 +4438,22 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     // two launches whose workgroups exit at once)
     uint8_t* redo = ws + W.redo;
     const uint32_t k2need = fork ? (a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS : 0;
-    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[0], s)) != hipSuccess) return e;
+    if ((e = dom(DOM_FUSED, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(zd_k_fused, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * FZ_WAVES), 0, s,
                        a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
                        fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
-    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[1], s)) != hipSuccess) return e;
+    if ((e = dom(DOM_FUSED, 1)) != hipSuccess) return e;
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, redo);
-    k4(0, a.n_frames, s, redo);
+    if ((e = k4(0, a.n_frames, s, redo)) != hipSuccess) return e;
   } else {
     k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, nullptr);
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
-    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[0], s)) != hipSuccess) return e;
-    k4(0, a.n_frames, s, nullptr);
-    if (a.dom_events) if ((e = hipEventRecord(a.dom_events[1], s)) != hipSuccess) return e;
-    k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s);
+    if ((e = k4(0, a.n_frames, s, nullptr)) != hipSuccess) return e;
+    if ((e = k4f((const uint32_t*)(ws + W.list_k4f), a.n_k4f, s)) != hipSuccess) return e;
   }
   if (a.events) if ((e = hipEventRecord(a.events[5], s)) != hipSuccess) return e;
   if (a.n_jframes) {
@@ -4454,6 +4464,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     auto* jsd = (const JSegDesc*)(ws + W.jsegd);
     auto* jst = (uint32_t*)(ws + W.jst);
     auto* pend = (uint32_t*)(ws + W.jpend);
+    if ((e = dom(DOM_K4J, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(zd_k_jsum, dim3(a.n_jseg), dim3(64), 0, s, a.src, (const FrameState*)fstate, blocks, comp,
                        (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jsd, jseg);
     hipLaunchKernelGGL(zd_k_jsum_blocks, dim3((a.n_jblk + 63) / 64), dim3(64), 0, s, (const FrameState*)fstate,
@@ -4471,6 +4482,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     for (uint32_t r = 1; r <= a.j_rounds; r++)
       hipLaunchKernelGGL(zd_k_jround, r <= 2 ? gr : gt, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
                          a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == a.j_rounds));
+    if ((e = dom(DOM_K4J, 1)) != hipSuccess) return e;
   }
   if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;
   return hipGetLastError();

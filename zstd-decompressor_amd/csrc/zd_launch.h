@@ -27,10 +27,12 @@ struct LaunchArgs {
   bool fused = false;                      // K3 + K4 as zd_k_fused, then the redo pass
   bool k1_seq_waves = false;               // K1's sequence half one wave per block (zd_k_tables_seqw)
   bool k1_fork = false;                    // no K2 | K3 fork: K1's halves on the two streams (aux, fork, join)
-  // optional: two events recorded on `stream` around the pipeline's dominant
-  // launch as it runs (zd_k_fused in fused plans, else zd_k_execute), with
-  // the fork and fusion kept (zd_plan_set_profiling mode 2)
+  // optional (zd_plan_set_profiling mode 2): an event pair recorded on
+  // `stream` around each launch group that can carry a plan's work -- K0,
+  // zd_k_fused, K4, K4F, the K4J kernels (kDomNames) -- with the fork and
+  // fusion kept; bit g of *dom_used is set when group g launched
   hipEvent_t* dom_events = nullptr;
+  uint32_t* dom_used = nullptr;
 };
 
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
@@ -65,6 +67,10 @@ hipError_t launch_plan_fill(const PlanCtx& X, const HostFrame* frames, const Hos
                             const uint64_t* cnt, const uint64_t* tot, const Sink& S, hipStream_t s);
 
 constexpr int N_KERNELS = 6;
+// mode-2 launch groups (LaunchArgs::dom_events: events 2g, 2g + 1)
+constexpr int N_DOM = 5;
+enum { DOM_K0 = 0, DOM_FUSED = 1, DOM_K4 = 2, DOM_K4F = 3, DOM_K4J = 4 };
+extern const char* const kDomNames[N_DOM];
 constexpr uint32_t K4F_CAP = K4F_CAP_BYTES;   // frames up to this output size execute in LDS (K4F)
 extern const char* const kKernelNames[N_KERNELS];
 

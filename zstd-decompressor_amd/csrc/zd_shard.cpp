@@ -179,6 +179,13 @@ int zd_comm_create(const uint8_t id[ZD_COMM_ID_BYTES], int world, int rank, zd_c
   return ZD_OK;
 }
 
+int zd_comm_buffers(const zd_comm* c, uint64_t* src_bytes, uint64_t* out_bytes) {
+  if (!c) return ZD_E_INVALID_ARG;
+  if (src_bytes) *src_bytes = c->src_cap;
+  if (out_bytes) *out_bytes = c->out_cap;
+  return ZD_OK;
+}
+
 void zd_comm_destroy(zd_comm* c) {
   if (!c) return;
   Rccl* R = rccl();

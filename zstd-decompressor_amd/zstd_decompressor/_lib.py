@@ -90,6 +90,7 @@ SIGNATURES = {
     "zd_comm_unique_id": (C.c_int, [_vp]),
     "zd_comm_create": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_vp)]),
     "zd_comm_destroy": (None, [_vp]),
+    "zd_comm_buffers": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "zd_gather_layout": (C.c_int, [C.POINTER(C.c_int64), C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                    C.POINTER(GatherResult)]),
     "zd_comm_gather": (C.c_int, [_vp, _vp, C.c_uint64, C.c_int32, C.c_int64, _vp, C.c_uint64,
