@@ -294,6 +294,9 @@ def main():
                          "(auto: on for strong scaling)")
     ap.add_argument("--no-host-io", action="store_true",
                     help="skip the host-in / host-out leg (profiling runs of the device path)")
+    ap.add_argument("--share", default=None, metavar="R/N",
+                    help="one GPU, one process: decode only rank R's frame range of the N-way strong partition "
+                         "(the share one rank of an N-GPU run decodes, measured alone; no gather)")
     ap.add_argument("--experiment", action="store_true",
                     help="timing-only variants: do not stop on decode errors")
     args = ap.parse_args()
@@ -313,7 +316,10 @@ def main():
     from zstd_decompressor.batch import Plan, frames_index
 
     # ---- corpus (host) ----
-    strong = world > 1 and args.scaling == "strong" and args.workload != "c3s"
+    # --share R/N: this process plays rank R of an N-way strong split
+    prank, pworld = (int(args.share.split("/")[0]), int(args.share.split("/")[1])) if args.share else (rank, world)
+    assert world == 1 or not args.share, "--share is a one-process option"
+    strong = pworld > 1 and args.scaling == "strong" and args.workload != "c3s"
     seed = 0x5EED + (0 if (strong or world == 1) else 7919 * rank)
     cache = None
     if args.corpus_cache:
@@ -336,8 +342,8 @@ def main():
     n_global = len(set_frames) * reps
     if strong:
         # one corpus, contiguous frame ranges balanced by compressed bytes
-        ranges = shard.partition([set_frames[k % len(set_frames)]["src_size"] for k in range(n_global)], world)
-        fb, fe = ranges[rank]
+        ranges = shard.partition([set_frames[k % len(set_frames)]["src_size"] for k in range(n_global)], pworld)
+        fb, fe = ranges[prank]
         data, ref_bytes = shard_bytes(frame_set, set_frames, src, reps, fb, fe)
     else:
         fb, fe = 0, n_global
@@ -548,6 +554,8 @@ def main():
                     f"{args.unique_mib} MiB unique x{reps}"}[args.workload]
         if world > 1:
             wl += (f", frame-sharded across {world} GPUs" if strong else f", one such corpus per GPU ({world})")
+        if args.share:
+            wl += f", rank {prank}'s share of a {pworld}-way frame split, decoded alone on one GPU"
         res = {
             "metric": "decompressed MB/s (bit-exact vs ref) + % HBM roofline",
             "value": round(value, 1),
@@ -576,7 +584,8 @@ def main():
                                  "real enwik text at ~3.5-4x at these levels (SURVEY.md Appendix A), so each output "
                                  "byte here carries more sequences and literals than enwik9's would; value and "
                                  "roofline.frac are not directly comparable to a real-enwik run",
-                "parallelism": f"frame-sharded x{world}" if strong else f"replicas x{world}",
+                "parallelism": (f"share {prank}/{pworld} alone" if args.share else
+                                f"frame-sharded x{world}" if strong else f"replicas x{world}"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -48,6 +48,10 @@ for s in "$@"; do
     pmchbm10) run pmc_fetch10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_fetch10 -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io && run pmc_write10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_write10 -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io ;;
     benchc5:*) l=${s#benchc5:}; run bench_c5_L$l 900 python bench.py --workload c5 --level $l --no-host-io ;;
     benchc2) run bench_c2 600 python bench.py --workload c2 ;;
+    benchc2big) run bench_c2_1GiB 600 python bench.py --workload c2 --c2-mib 1024 --no-cpu-baseline ;;
+    profc2big) run prof_c2_1GiB 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2big -o run --output-format csv -- python bench.py --workload c2 --c2-mib 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-host-io ;;
+    share:*) x=${s#share:}; run bench_share_${x//\//of} 600 python bench.py --share $x --no-cpu-baseline --no-host-io ;;
+    testshard) run pytest_shard 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu tests/test_shard.py ;;
     env:*) e=${s#env:}; run bench_env_${e//[=,]/_} 600 env ${e//,/ } python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     var:*) v=${s#var:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run bench_var_$v 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     *) echo "unknown step $s"; exit 2 ;;
