@@ -2322,6 +2322,10 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 #ifndef ZD_K4_INWIN
 #define ZD_K4_INWIN 1
 #endif
+#ifndef ZD_K4_OVS
+#define ZD_K4_OVS 0                         // pass 0: merged 16-byte chunks written past their end
+#endif
+constexpr int K4_WPAD = ZD_K4_OVS ? 16 : 0;  // LDS bytes below the window
 #ifndef ZD_K4_STG
 #define ZD_K4_STG 512                       // C4, 4 GiB: 1024 8.36 ms, 512 8.25, 256 8.24
 #endif
@@ -2641,11 +2645,27 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
         const bool far = valid && lane < kk && ml && off32 >= 16 && off32 <= (uint32_t)q &&
                          shi <= (X.hs < fl_safe ? X.hs : fl_safe);
+#if ZD_K4_OVS
+        // pass 0 (below) writes each lane's sequence as 16-byte chunks that
+        // merge its literal and match bytes; a far lane's first two chunks'
+        // match bytes are loaded now (chunk b reads the source at slo + b - ll,
+        // so the match bytes land at chunk offset ll - b; a chunk of literal
+        // bytes only reads at slo)
+        u32x4 fv0, fv1;
+        const bool far0 = far && slo >= 16;
+        const uint32_t n0f = ll + ml;
+        const uint32_t bb1 = n0f >= 32 ? 16u : (n0f > 16 ? n0f - 16 : 0u);
+        if (far0) {
+          fv0 = ldg16_src(X.out + (uint32_t)(ll >= 16 ? slo : slo - (int32_t)ll));
+          if (n0f > 16) fv1 = ldg16_src(X.out + (uint32_t)(ll >= bb1 + 16 ? slo : slo + (int32_t)bb1 - (int32_t)ll));
+        }
+#else
         u32x4 fv0, fv1;
         if (far) {
           fv0 = ldg16_src(X.out + (uint32_t)slo);
           if (ml > 16) fv1 = ldg16_src(X.out + (uint32_t)(slo + 16));
         }
+#endif
         // matches whose source lies wholly in the window and before this
         // batch (written by earlier batches, so no order among the lanes):
         // copied from LDS in the same pass as the far ones, not in rounds.
@@ -2683,6 +2703,63 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, s0, ZD_E_OUT_OF_DOMAIN); break; }
         const bool act = (uint32_t)lane < k;
         k4_sync();                               // staged literals visible
+#if ZD_K4_OVS
+        // Pass 0: every executing lane writes its bytes as 16-byte chunks at
+        // its output start: the whole sequence (literals then match) when
+        // the match source lies before this batch (far: HBM, inwin: window)
+        // or there is no match, else its literals only (the match follows in
+        // the frontier rounds).  Chunks start every 16 bytes and the last one
+        // ends exactly at the lane's end, so only a lane writing fewer than 16
+        // bytes writes past its end: into later lanes' bytes, which this same
+        // store rewrites (LDS: within one wave's ds_write, the highest lane
+        // writing a byte wins -- tools/lds_order_check, test_lds_write_order)
+        // or which the lanes' own later writes cover (a literals-only lane's
+        // match, a lane with literals past the stage).  A chunk takes
+        // ll - b literal bytes (from the stage) then match bytes read at
+        // slo + b - ll: the bytes before slo are never used, and the window
+        // keeps 16 bytes of padding below its start for them.
+        const bool lslow = act && ll && lit_stage && lpos + ll > K4_STG;
+        const bool full0 = act && !lslow && (ml == 0 || far0 || inwin);
+        const uint32_t n0 = (act && !lslow) ? (full0 ? ll + ml : ll) : 0u;
+        if (n0) {
+          l_u8* d = X.at(X.pos + (int32_t)opos);
+          const uint32_t last = n0 >= 16 ? n0 - 16 : 0u;
+          const bool src_far = full0 && far0;
+          const bool src_win = full0 && inwin;
+          for (uint32_t b0 = 0, it = 0;; b0 += 16, it++) {
+            const uint32_t bb = min(b0, last);
+            const uint32_t kl = ll > bb ? min(ll - bb, 16u) : 0u;      // literal bytes in the chunk
+            u32x4 lv = f4;
+            if (lit_stage) lv = lds16((const l_u8*)stg + min(lpos + bb, K4_STG));
+            u32x4 mv = lv;
+            if (kl < 16) {
+              const int32_t ma = slo + (int32_t)bb - (int32_t)ll;
+              if (src_far) mv = it == 0 ? fv0 : it == 1 ? fv1 : ldg16_src(X.out + (uint32_t)ma);
+              else if (src_win) mv = lds16(X.at(ma));
+            }
+            // bytes [0, kl) from lv, the rest from mv
+            const uint64_t mlo = kl >= 8 ? ~0ull : ((1ull << (8 * kl)) - 1);
+            const uint64_t mhi = kl >= 16 ? ~0ull : (kl <= 8 ? 0ull : ((1ull << (8 * (kl - 8))) - 1));
+            u32x4 v;
+            v.x = ((uint32_t)mlo & lv.x) | (~(uint32_t)mlo & mv.x);
+            v.y = ((uint32_t)(mlo >> 32) & lv.y) | (~(uint32_t)(mlo >> 32) & mv.y);
+            v.z = ((uint32_t)mhi & lv.z) | (~(uint32_t)mhi & mv.z);
+            v.w = ((uint32_t)(mhi >> 32) & lv.w) | (~(uint32_t)(mhi >> 32) & mv.w);
+            *(l_u32x4a1*)(d + bb) = v;
+            if (b0 + 16 >= n0) break;
+          }
+        }
+        if (__ballot(lslow)) {                         // literals past the stage: exact, from HBM
+          if (lslow) {
+            l_u8* d = X.at(X.pos + (int32_t)opos);
+            for (uint32_t x = 0; x < ll; x += 16) sts_n(d + x, ldg16(lsrc + lit_cursor + lpos + x), ll - x);
+          }
+        }
+        K4_PHASE(2);
+        K4_PHASE(3);
+        if (__ballot(act && ml && !full0 && slo < X.hs)) wait_vm();
+        uint64_t done = __ballot(!act || full0);
+#else
         // literals (every lane its own run; from the stage when it holds them)
         if (act && ll) {
           l_u8* d = X.at(X.pos + (int32_t)opos);
@@ -2729,6 +2806,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         }
         if (__ballot(act && ml && !far && slo < X.hs)) wait_vm();
         uint64_t done = __ballot(!act || ml == 0 || far || inwin);
+#endif
         k4_sync();
         K4_PHASE(3);
         while (done != ~0ull) {
@@ -2821,12 +2899,13 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
                                                    const uint64_t* __restrict__ seqs,
                                                    const uint16_t* __restrict__ fses, uint32_t f_begin,
                                                    uint32_t f_end, const uint8_t* __restrict__ redo) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[K4_C];
+  // (16 bytes of padding below the window: pass 0 reads up to 15 bytes before a match source)
+  __shared__ __attribute__((aligned(16))) uint8_t win[K4_WPAD + K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[3 * FSE_TAB];   // LL | OF | ML symbols of the block
   __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
   __shared__ uint32_t codelut[2 * 64];
-  const K4Lds M{(l_u8*)win, (l_u8*)pat, (l_u8*)stab, (l_u8*)stg, (l_u32*)codelut};
+  const K4Lds M{(l_u8*)win + K4_WPAD, (l_u8*)pat, (l_u8*)stab, (l_u8*)stg, (l_u32*)codelut};
   k4_body<false>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f_begin + blockIdx.x, f_end,
                  gridDim.x, redo, M, nullptr, nullptr);
 }
@@ -3085,7 +3164,7 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
     const uint8_t* __restrict__ lits, uint64_t* __restrict__ seqs, uint16_t* __restrict__ fses,
     uint32_t n_frames, const uint32_t* k2done, uint32_t k2need, uint8_t* redo) {
   __shared__ __attribute__((aligned(16))) uint16_t tabs[FZ_FRAMES * K3_TAB];
-  __shared__ __attribute__((aligned(16))) uint8_t win[FZ_FRAMES][K4_C];
+  __shared__ __attribute__((aligned(16))) uint8_t win[FZ_FRAMES][K4_WPAD + K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[FZ_FRAMES][64];
   __shared__ __attribute__((aligned(16))) uint8_t stab[FZ_FRAMES][3 * FSE_TAB];
   __shared__ __attribute__((aligned(16))) uint8_t stg[FZ_FRAMES][K4_STG + 16];
@@ -3126,7 +3205,7 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
       if (lane == 0) FZT(f, 1);
       k4_sync();
     }
-    const K4Lds M{(l_u8*)win[q], (l_u8*)pat[q], (l_u8*)stab[q], (l_u8*)stg[q], (l_u32*)codelut[q]};
+    const K4Lds M{(l_u8*)win[q] + K4_WPAD, (l_u8*)pat[q], (l_u8*)stab[q], (l_u8*)stg[q], (l_u32*)codelut[q]};
     const K4Fuse z{(const volatile l_u32*)&prog[q], (const volatile l_u32*)&trdy[q], k2done, k2need, f};
     k4_body<true>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f, f + 1, 1, nullptr, M, &z,
                   redo);
