@@ -2452,7 +2452,11 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
     for (int32_t p = (X.hs > 0 ? X.hs : 0) + lane; p < X.pos; p += 64) *X.at(p) = X.out[p];
     k4_sync();
   }
-  uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
+  // repeat offsets in 32 bits: every offset a frame can use without an
+  // ImpossibleValue is below 2^31 (a position), and a larger one stops the
+  // frame at its sequence, so saturating at 2^32 - 1 keeps every outcome
+  auto sat32 = [](uint64_t v) -> uint32_t { return v < 0xFFFFFFFFull ? (uint32_t)v : 0xFFFFFFFFu; };
+  uint32_t rep[3] = {sat32(S->rep[0]), sat32(S->rep[1]), sat32(S->rep[2])};
   uint64_t err_key = abandoned ? 0 : KEY_NONE;
   // HBM holds [0, fl_safe) with every store completed (the bytes two batches
   // back); fl_last = the flush boundary after the previous batch
@@ -2535,7 +2539,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       u32x4 litA = lit_of(lit_cursor);
       bool big = false;                              // batch loop left for one large sequence
       uint32_t bll = 0, bml = 0;
-      uint64_t boff = 0;
+      uint32_t boff = 0;
       for (;;) {
         const uint32_t i = s0 + lane;
         const bool valid = i < vlim;
@@ -2579,12 +2583,21 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
             ll_code(llc, &llbase, &llb);
             ml_code(mlc, &mlbase, &mlb);
 #endif
-            {
-            uint64_t t = winu_top(winA, 0);
-            const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
-            ofv = (1u << ofc) + ob;
-            ml = mlbase + mb;
-            ll = llbase + lb;
+            // the OF, ML, LL extra bits MSB-first below the position: from
+            // the top 32 bits when the batch's fit them (three bit-field
+            // extracts), else from the top 64
+            const uint32_t S3 = ofc + mlb + llb;
+            if (__ballot(S3 > 32 || winA.sh > 32) == 0) {
+              const uint32_t t32 = (uint32_t)((winA.w1 << winA.sh) >> 32);
+              ofv = (1u << ofc) + __builtin_amdgcn_ubfe(t32, 32 - ofc, ofc);
+              ml = mlbase + __builtin_amdgcn_ubfe(t32, 32 - ofc - mlb, mlb);
+              ll = llbase + __builtin_amdgcn_ubfe(t32, 32 - S3, llb);
+            } else {
+              uint64_t t = winu_top(winA, 0);
+              const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
+              ofv = (1u << ofc) + ob;
+              ml = mlbase + mb;
+              ll = llbase + lb;
             }
           }
         }
@@ -2604,42 +2617,61 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         // are direct; the rare repeat codes walk the batch in order on the
         // scalar unit, each from the state the fresh offsets before it left.
         const bool fresh = ofv > 3;
-        const uint64_t val = giant ? OFF_HUGE : (uint64_t)ofv - 3;
-        uint64_t off = val;
+        // off32: a fresh lane's offset (offset_value - 3; 2^32 - 1 for the
+        // context API's giant values), a repeat lane's once the walk set it
+        uint32_t off32 = giant ? 0xFFFFFFFFu : ofv - 3;
         int derr = 0;
         uint64_t rm = __ballot(valid && !fresh && lane < kk);
-        uint64_t r0 = rep[0], r1 = rep[1], r2 = rep[2];   // state after lane `prev`
+        // state after lane `prev` (uniform: readfirstlane keeps the walk on the scalar unit)
+        uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rep[0]);
+        uint32_t r1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rep[1]);
+        uint32_t r2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rep[2]);
         int prev = -1;
+        // a repeat lane's code (offset_value 0..3) and whether its literals_length is 0
+        const uint32_t rcode = (ofv & 3) | (ll != 0 ? 4u : 0u);
         while (rm) {
           const int ri = __ffsll((long long)rm) - 1;
           rm &= rm - 1;
-          uint64_t a0, a1, a2;
-          rep_push(val, ri - prev - 1, ri, r0, r1, r2, &a0, &a1, &a2);
-          const uint32_t oi = (uint32_t)__builtin_amdgcn_readlane((int)ofv, ri);
-          const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)ll, ri);
-          uint64_t o = 0;
+          // the fresh lanes between prev and ri pushed their values (at most the last three count)
+          const int cnt = ri - prev - 1;
+          uint32_t a0 = r0, a1 = r1, a2 = r2;
+          if (cnt >= 1) { a0 = (uint32_t)__builtin_amdgcn_readlane((int)off32, ri - 1); a1 = r0; a2 = r1; }
+          if (cnt >= 2) { a1 = (uint32_t)__builtin_amdgcn_readlane((int)off32, ri - 2); a2 = r0; }
+          if (cnt >= 3) a2 = (uint32_t)__builtin_amdgcn_readlane((int)off32, ri - 3);
+          const uint32_t ci = (uint32_t)__builtin_amdgcn_readlane((int)rcode, ri);
+          const uint32_t oi = ci & 3;
+          uint32_t o = 0;
           int e = 0;
           if (oi == 0) {
             e = ZD_E_NULL_OFFSET;
           } else {
-            const uint32_t idx = oi - (li != 0 ? 1u : 0u);
+            const uint32_t idx = oi - ((ci & 4) ? 1u : 0u);
             if (idx == 0) { o = a0; }
             else if (idx == 1) { o = a1; a1 = a0; a0 = o; }
             else if (idx == 2) { o = a2; a2 = a1; a1 = a0; a0 = o; }
             else if (a0 == 0) { e = ZD_E_REF_PANIC; }     // usize underflow of offsets[0] -= 1
             else { o = a0 - 1; a2 = a1; a1 = a0; a0 = o; }
           }
-          if (lane == ri) { off = o; derr = e; }
+          off32 = lane == ri ? o : off32;
+          derr = lane == ri ? e : derr;
           r0 = a0; r1 = a1; r2 = a2;
           prev = ri;
           if (e) break;                                // the frame stops at this sequence
         }
+        // the repeat state after lane end - 1, the lanes after prev fresh
+        auto rep_after = [&](int end) {
+          const int c = end - 1 - prev;
+          uint32_t b0 = r0, b1 = r1, b2 = r2;
+          if (c >= 1) { b0 = (uint32_t)__builtin_amdgcn_readlane((int)off32, end - 1); b1 = r0; b2 = r1; }
+          if (c >= 2) { b1 = (uint32_t)__builtin_amdgcn_readlane((int)off32, end - 2); b2 = r0; }
+          if (c >= 3) b2 = (uint32_t)__builtin_amdgcn_readlane((int)off32, end - 3);
+          rep[0] = b0; rep[1] = b1; rep[2] = b2;
+        };
         K4_PHASE(1);
         // matches whose source lies wholly in HBM, flushed two batches ago or
         // earlier (those stores completed before this batch's waits): their
         // first 32 source bytes are loaded now, to land during the checks
         // and the literal copies
-        const uint32_t off32 = (uint32_t)(off < 0xFFFFFFFFull ? off : 0xFFFFFFFFull);
         const int32_t q = X.pos + (int32_t)(opos + ll);
         const int32_t slo = q - (int32_t)off32;
         const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
@@ -2694,8 +2726,8 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
           big = true;
           bll = (uint32_t)__builtin_amdgcn_readlane((int)ll, 0);
           bml = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0);
-          boff = readlane_u64(off, 0);
-          rep_push(val, 0 - prev, 1, r0, r1, r2, &rep[0], &rep[1], &rep[2]);
+          boff = (uint32_t)__builtin_amdgcn_readlane((int)off32, 0);
+          rep_after(1);
           break;
         }
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
@@ -2838,7 +2870,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
 #ifdef ZD_K4_PROF
         nb++;
 #endif
-        rep_push(val, (int)k - 1 - prev, (int)k, r0, r1, r2, &rep[0], &rep[1], &rep[2]);   // state after lane k - 1
+        rep_after((int)k);                             // state after lane k - 1
         lit_cursor += L;
         X.pos += (int32_t)T;
         s0 += k;
@@ -2850,7 +2882,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       if (big && err_key == KEY_NONE) {
         // one sequence larger than the window's room: the whole wave copies it
         if (!k4_emit_lits(X, lsrc ? lsrc + lit_cursor : nullptr, lfill, bll) ||
-            !k4_emit_match(X, (l_u8*)pat, (uint32_t)(boff < 0xFFFFFFFFull ? boff : 0xFFFFFFFFull), bml)) {
+            !k4_emit_match(X, (l_u8*)pat, boff, bml)) {
           err_key = make_key(PH_LIMIT, j, LS_CAPACITY, s0, ZD_E_OUT_OF_DOMAIN);
           break;
         }
