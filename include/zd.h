@@ -291,6 +291,15 @@ int zd_plan_kernel_times(zd_plan* plan, const char** names, float* ms, int cap, 
  * GPU; a caller that wants overlap uses zd_decode_async on its own streams.
  * One plan is not used from two threads at once. */
 int zd_plan_decompress(zd_plan* plan, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
+/* Per-frame outcome of the last zd_plan_decompress on the plan (its re-plans
+ * included): frame f's status (ZD_OK, the frame's error, or
+ * ZD_E_NOT_DECODED after the first failing frame) and where its bytes sit in
+ * dst (offset, length; length 0 unless ZD_OK).  *n = the plan's frames
+ * (0 before any call); arrays of cap entries, any may be NULL.  This is what
+ * a FrameIterator-style caller (frame.rs:86-99) hands out frame by frame
+ * from one decode of the whole buffer. */
+int zd_plan_frame_outputs(const zd_plan* plan, int32_t* status, uint64_t* offset, uint64_t* length, size_t cap,
+                          size_t* n);
 /* Convenience: host in, host out (H2D + decode + D2H on the default
  * stream).  Mirrors the CLI (src/main.rs:43-58) minus the UTF-8 step. */
 int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap,

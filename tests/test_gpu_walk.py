@@ -99,8 +99,10 @@ def test_device_descriptors(tmp_path):
     zd_plan.h) and reads back only the totals and the frames' output offsets
     and capacities (info.device_descriptors).  The plan equals the host
     planner's descriptor for descriptor, with and without -p, and decodes the
-    same; a C4-shaped plan of 2,048 single-block frames and the host-walk
-    inputs with skippable frames or a failing frame take that path."""
+    same; a C4-shaped plan of 2,048 single-block frames, the host-walk inputs
+    with skippable frames or a failing frame, and plans with K4J frames (a
+    single frame of many blocks, few multi-block frames, 16-block frames in a
+    larger plan) take that path."""
     import torch
     import test_host_walk
     from zstd_decompressor.batch import Plan
@@ -110,6 +112,15 @@ def test_device_descriptors(tmp_path):
     cases = [("c4 x4", c4 * 4, True), ("intact", inputs["intact"], True), ("skippable", inputs["skippable"], True)]
     for i in range(6):
         cases.append((f"corrupt {i}", inputs[f"corrupt {i}"], False))
+    # plans with K4J frames (round 5: their descriptors are built on the GPU
+    # too): a c3s-shaped single frame of many blocks, a plan of <= 64 frames
+    # of 2+ blocks each, and 16-block frames in a larger plan
+    from corpus import libzstd
+    big = gen.text(24 << 20, seed=95)
+    few = b"".join(gen.frames(big[i << 20:(i + 1) << 20], 1 << 20, 9) for i in range(6))
+    many = gen.frames(gen.text(80 << 20, seed=96), 2 << 20, 3) + c4[: len(c4) // 4]
+    cases += [("c3s-shaped single frame", libzstd.compress(big, 3), True), ("few multi-block frames", few, True),
+              ("16-block frames among single-block ones", many, True)]
     took = 0
     for name, data, must in cases:
         for skip in (False, True):
@@ -128,4 +139,4 @@ def test_device_descriptors(tmp_path):
                 assert _decode(dp, d_src, dev) == _decode(hp, d_src, dev), name
             hp.close()
             dp.close()
-    assert took >= 6
+    assert took >= 12

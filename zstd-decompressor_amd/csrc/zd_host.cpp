@@ -97,6 +97,7 @@ struct zd_plan {
   // a plan whose descriptors the GPU built (zd_plan_create_device): its
   // frame index stays in the workspace (W.hframes) until a caller needs it
   bool dev_built = false;
+  zd::FrameOuts io_fo;                   // per-frame outcome of the last zd_plan_decompress
   mutable std::vector<HostFrame> dev_frames;
   // the frame index on the host (a device-built plan's comes back once);
   // false when it cannot be read -- nothing is kept then, a later call retries
@@ -453,6 +454,12 @@ void plan_info(zd_plan* P, const PlanCounts& T) {
   I.executors = (P->fused ? ZD_EXEC_FUSED : 0u) | (P->n_k4f ? ZD_EXEC_K4F : 0u) | (P->n_jframes ? ZD_EXEC_K4J : 0u);
 }
 
+// The largest K4J frame's sequence count (plan_frame's jm)
+struct JMax {
+  uint64_t m = 0;
+  void note(uint64_t n) { m = std::max(m, n); }
+};
+
 // Builds device-side descriptors from the host frames: one counting pass and
 // one filling pass over the parts in parallel (each part's entries start at
 // the counts of the parts before it), then the K4J descriptors in frame order.
@@ -475,7 +482,7 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   run_parts(np, [&](size_t k) {
     const HostPart& hp = P->parts[k];
     PlanCounts c;
-    for (const HostFrame& hf : hp.frames) plan_frame<false, std::vector<uint32_t>>(X, hf, hp.blocks.data(), c, none, nullptr);
+    for (const HostFrame& hf : hp.frames) plan_frame<false, JMax>(X, hf, hp.blocks.data(), c, none, nullptr);
     if (X.fused) {          // parts start aligned, so the filling pass pads exactly as this count did
       c.lits = align_up(c.lits, 128);
       c.nrec = align_up(c.nrec, 16);
@@ -539,47 +546,16 @@ int build_plan(zd_plan* P, int32_t prev_huf, const int32_t prev_tab[3], uint64_t
   }
   S.frame_out = P->frame_out.data();
   S.frame_cap = P->frame_cap.data();
-  std::vector<std::vector<uint32_t>> jfr(np);
+  // (the K4J descriptors are written by plan_frame at the running K4J indices)
+  std::vector<JMax> jm(np);
   run_parts(np, [&](size_t k) {
     const HostPart& hp = P->parts[k];
     PlanCounts c = cnt[k];
-    for (const HostFrame& hf : hp.frames) plan_frame<true, std::vector<uint32_t>>(X, hf, hp.blocks.data(), c, S, &jfr[k]);
+    for (const HostFrame& hf : hp.frames) plan_frame<true, JMax>(X, hf, hp.blocks.data(), c, S, &jm[k]);
   });
-
-  // K4J descriptors, frames in order
-  uint64_t j_base = 0, j_pieces = 0, j_maxseq = 0;
-  uint32_t nj = 0, njb = 0, njs = 0;
-  for (const auto& part : jfr) {
-    for (uint32_t fi : part) {
-      const FrameDesc& fd = S.fdesc[fi];
-      JFrame jf{};
-      jf.base = align_up(j_base, 16);          // word index: frame pieces of 16 words are 64-byte lines
-      jf.cap = fd.out_cap;
-      jf.piece0 = j_pieces;
-      jf.frame = fi;
-      jf.jb0 = njb;
-      jf.njb = fd.nblocks;
-      uint64_t nseq = 0;
-      for (uint32_t k = 0; k < fd.nblocks; k++) {
-        JBlkDesc d{};
-        d.block = fd.first_block + k;
-        d.jframe = nj;
-        d.j = k;
-        d.seg0 = njs;
-        const BlockRec& br = S.blocks[fd.first_block + k];
-        const uint32_t bn = br.comp >= 0 ? S.comps[(size_t)br.comp].nseq : 0;
-        nseq += bn;
-        for (uint32_t g = 0; g == 0 || g * J_SEG < bn; g++) S.jsegd[njs++] = JSegDesc{njb, g};
-        S.jblkd[njb++] = d;
-      }
-      j_maxseq = std::max(j_maxseq, nseq);
-      j_base = jf.base + fd.out_cap + 16;
-      j_pieces += (fd.out_cap + 15) / 16;
-      S.jframes[nj++] = jf;
-    }
-  }
-
-  carve_tail(P, W, T, o, j_base, j_pieces, j_maxseq);
+  uint64_t j_maxseq = 0;
+  for (const JMax& m : jm) j_maxseq = std::max(j_maxseq, m.m);
+  carve_tail(P, W, T, o, T.jwords, T.jpieces, j_maxseq);
   W.total = o;
 
   plan_info(P, T);
@@ -1095,12 +1071,12 @@ void parts_from(const std::vector<const HostFrame*>& kept, const HostBlock* bl, 
 // plan's totals (PLAN_FIELDS words) and the frames' output offsets and
 // capacities (16 bytes a frame); everything else is written in place in the
 // workspace by the planner's own per-frame pass (zd_plan.h plan_frame).
-// Returns 1 when the plan needs the host's descriptors instead (K4J frames,
-// whose descriptors are listed in frame order on the host).
+// K4J frames included: plan_frame writes their descriptors at the scanned
+// K4J indices, and the count pass reports the largest K4J frame's sequence
+// count (the rounds), so no plan falls back to the host build.
 int build_plan_device(zd_plan* P, DevWalkBufs& B, uint64_t F, hipStream_t s) {
   const HostFrame* d_frames = (const HostFrame*)B.d_out;
   const HostBlock* d_blocks = (const HostBlock*)(B.d_out + B.fb);
-  if (k4j_mode_of(P->flags) == 1) return 1;
   P->nframes = F;
   const uint32_t k4j_min = F <= K4J_FEW_FRAMES ? K4J_MIN_BLOCKS_FEW : K4J_MIN_BLOCKS;
   const uint64_t nt = (F + 255) / 256;
@@ -1117,20 +1093,20 @@ int build_plan_device(zd_plan* P, DevWalkBufs& B, uint64_t F, hipStream_t s) {
   const int32_t none[3] = {-1, -1, -1};
   const uint64_t rep0[3] = {1, 4, 8};
   const PlanCtx X = plan_ctx(P, -1, none, 0, rep0, 0, shape.multi == 0, k4j_mode_of(P->flags) < 0 ? shape.jcand : 0);
-  if (X.k4j_auto) return 1;                     // some frame goes to K4J
-  HIPCHK(launch_plan_count(X, d_frames, d_blocks, F, B.d_cnt, B.d_tot, s));
+  HIPCHK(launch_plan_count(X, d_frames, d_blocks, F, B.d_cnt, B.d_tot, B.d_shape, s));
   HIPCHK(hipMemcpyAsync(B.h_small, B.d_tot + nt * PLAN_FIELDS, PLAN_FIELDS * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(B.h_small + PLAN_FIELDS, B.d_shape, sizeof(PlanShape), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   PlanCounts T;
   memcpy(&T, B.h_small, sizeof T);
-  if (T.jframes) return 1;
+  memcpy(&shape, B.h_small + PLAN_FIELDS, sizeof shape);
   Workspace& W = P->W;
   W = Workspace{};
   uint64_t o = 0;
   carve_head(W, T, o);
   P->desc_bytes = o;
   plan_totals(P, T, X.fused);
-  carve_tail(P, W, T, o, 0, 0, 0);
+  carve_tail(P, W, T, o, T.jwords, T.jpieces, shape.jmaxseq);
   W.hframes = o;
   o = align_up(o + sizeof(HostFrame) * std::max<uint64_t>(F, 1), 256);
   W.total = o;
@@ -1835,7 +1811,7 @@ bool call_failed(int st) { return st == ZD_E_HIP || st == ZD_E_INVALID_ARG || st
 constexpr int LIMIT_RETRIES = 12;
 
 int zd::decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t* d_src, DevOut& out, void* stream,
-                        uint64_t* total_out, int64_t* first_out, uint64_t* replans) {
+                        uint64_t* total_out, int64_t* first_out, uint64_t* replans, FrameOuts* fo) {
   const hipStream_t s = (hipStream_t)stream;
   *total_out = 0;
   *first_out = -1;
@@ -1845,8 +1821,33 @@ int zd::decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t*
   if (st) return st;
   uint64_t produced = 0;
   int32_t first = -1;
-  st = zd_plan_results(P, out.p, s, nullptr, nullptr, &produced, &first);
+  // per-frame outcomes: the current plan's, written into fo from frame fbase on
+  std::vector<int32_t> fs;
+  std::vector<uint64_t> fl;
+  auto want = [&](zd_plan* Q) {
+    if (!fo) return;
+    fs.assign(Q->n_frames, 0);
+    fl.assign(Q->n_frames, 0);
+  };
+  auto keep = [&](zd_plan* Q, int64_t fb, uint64_t at) {
+    if (!fo) return;
+    uint64_t o = at;
+    for (size_t f = 0; f < Q->n_frames && fb + (int64_t)f < (int64_t)fo->status.size(); f++) {
+      fo->status[fb + f] = fs[f];
+      fo->off[fb + f] = o;
+      fo->len[fb + f] = fl[f];
+      o += fl[f];
+    }
+  };
+  if (fo) {
+    fo->status.assign(P->n_frames, ZD_E_NOT_DECODED);
+    fo->off.assign(P->n_frames, 0);
+    fo->len.assign(P->n_frames, 0);
+  }
+  want(P);
+  st = zd_plan_results(P, out.p, s, fo ? fs.data() : nullptr, fo ? fl.data() : nullptr, &produced, &first);
   if (call_failed(st)) return st;
+  keep(P, 0, 0);
   zd_plan* cur = P;
   size_t base = 0;                                 // cur's input starts at src + base
   int64_t fbase = 0;                               // and its frame 0 is P's frame fbase
@@ -1873,13 +1874,15 @@ int zd::decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t*
     int32_t qfirst = -1;
     st = devout_reserve(out, produced + qob, produced, s);
     if (!st) st = zd_decode_async(Q, d_src + at, out.p + produced, qob, s);
-    if (!st) st = zd_plan_results(Q, out.p + produced, s, nullptr, nullptr, &t2, &qfirst);
+    want(Q);
+    if (!st) st = zd_plan_results(Q, out.p + produced, s, fo ? fs.data() : nullptr, fo ? fl.data() : nullptr, &t2, &qfirst);
     if (cur != P) zd_plan_destroy(cur);
     cur = Q;
     base = at;
     fbase += (int64_t)f;
     first = qfirst;
     if (call_failed(st)) break;
+    keep(Q, fbase, produced);
     produced += t2;
   }
   if (cur != P) {
@@ -1910,7 +1913,7 @@ int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, s
   uint64_t produced = 0;
   int64_t first = -1;
   P->info.replans = 0;
-  const int st = decode_resident(P, src, n, P->io_src, o, s, &produced, &first, &P->info.replans);
+  const int st = decode_resident(P, src, n, P->io_src, o, s, &produced, &first, &P->info.replans, &P->io_fo);
   if (call_failed(st)) return st;
   const auto t2 = std::chrono::steady_clock::now();
   const size_t copy = (size_t)std::min<uint64_t>(produced, cap);
@@ -1924,6 +1927,19 @@ int zd_plan_decompress(zd_plan* P, const uint8_t* src, size_t n, uint8_t* dst, s
   if (out_len) *out_len = (size_t)produced;
   if (!st && produced > cap) return ZD_E_DST_TOO_SMALL;
   return st;
+}
+
+int zd_plan_frame_outputs(const zd_plan* P, int32_t* status, uint64_t* offset, uint64_t* length, size_t cap,
+                          size_t* n) {
+  if (!P) return ZD_E_INVALID_ARG;
+  const size_t m = P->io_fo.status.size();
+  for (size_t f = 0; f < m && f < cap; f++) {
+    if (status) status[f] = P->io_fo.status[f];
+    if (offset) offset[f] = P->io_fo.off[f];
+    if (length) length[f] = P->io_fo.len[f];
+  }
+  if (n) *n = m;
+  return ZD_OK;
 }
 
 int zd_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len, uint32_t flags) {

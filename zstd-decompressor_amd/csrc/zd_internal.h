@@ -36,7 +36,14 @@ struct DevOut {
 // failure, *first_frame = that frame's index in P (-1 if none), *replans =
 // re-plans made.  Returns the input's status (ZD_E_HIP / ZD_E_INVALID_ARG /
 // ZD_E_DST_TOO_SMALL: the call itself failed).
+// Per-frame outcome of a decode_resident call (optional): frame f of P's
+// status (ZD_OK, its error, ZD_E_NOT_DECODED after the first failure) and
+// its bytes' offset and length in the output, re-plans included.
+struct FrameOuts {
+  std::vector<int32_t> status;
+  std::vector<uint64_t> off, len;
+};
 int decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t* d_src, DevOut& out, void* stream,
-                    uint64_t* total, int64_t* first_frame, uint64_t* replans);
+                    uint64_t* total, int64_t* first_frame, uint64_t* replans, FrameOuts* fo = nullptr);
 
 }  // namespace zd

@@ -4782,14 +4782,16 @@ __global__ __launch_bounds__(64) void zd_k_walk(const uint8_t* __restrict__ src,
 // per-frame pass (zd_plan.h plan_frame, the host planner's own code) over the
 // device walk's frame / block index, one lane per frame.  A shape pass (the
 // plan-wide inputs of routing: frames that are not single-block zstd frames,
-// K4J candidates), a count pass (each frame's PlanCounts from zero), an
+// K4J candidates), a count pass (each frame's PlanCounts from zero, and the
+// largest K4J frame's sequence count), an
 // exclusive scan over frames (per 256-frame tile, then the tiles), and a fill
 // pass that writes CompBlock / BlockRec / FrameDesc / FrameState, the work
-// lists and K0's pieces straight into the plan's workspace.  Only the plan's
+// lists, K0's pieces and the K4J descriptors straight into the plan's workspace.  Only the plan's
 // totals and the frames' output offsets and capacities go back to the host.
 // ---------------------------------------------------------------------------
-struct DevJNone {            // K4J frames are listed by the host planner only
-  __device__ void push_back(uint32_t) {}
+struct DevJMax {              // the largest K4J frame's sequence count (PlanShape::jmaxseq)
+  unsigned long long* m;
+  __device__ void note(uint64_t n) { if (n) atomicMax(m, (unsigned long long)n); }
 };
 __global__ __launch_bounds__(256) void zd_k_plan_shape(const HostFrame* __restrict__ frames, uint64_t nf,
                                                        uint32_t k4j_min, PlanShape* out) {
@@ -4808,12 +4810,13 @@ __global__ __launch_bounds__(256) void zd_k_plan_shape(const HostFrame* __restri
 }
 __global__ __launch_bounds__(256) void zd_k_plan_count(PlanCtx X, const HostFrame* __restrict__ frames,
                                                        const HostBlock* __restrict__ blocks, uint64_t nf,
-                                                       PlanCounts* cnt) {
+                                                       PlanCounts* cnt, PlanShape* shape) {
   const uint64_t f = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (f >= nf) return;
   PlanCounts c{};
   const Sink none{};
-  plan_frame<false, DevJNone>(X, frames[f], blocks, c, none, nullptr);
+  DevJMax jm{(unsigned long long*)&shape->jmaxseq};
+  plan_frame<false, DevJMax>(X, frames[f], blocks, c, none, &jm);
   cnt[f] = c;
 }
 // Exclusive scan of the PlanCounts words over frames, in place: tile t's
@@ -4858,7 +4861,7 @@ __global__ __launch_bounds__(256) void zd_k_plan_fill(PlanCtx X, const HostFrame
   PlanCounts c;
   uint64_t* cw = (uint64_t*)&c;
   for (int w = 0; w < PLAN_FIELDS; w++) cw[w] = cnt[f * PLAN_FIELDS + w] + tot[(uint64_t)blockIdx.x * PLAN_FIELDS + w];
-  plan_frame<true, DevJNone>(X, frames[f], blocks, c, S, nullptr);
+  plan_frame<true, DevJMax>(X, frames[f], blocks, c, S, (DevJMax*)nullptr);
 }
 
 hipError_t launch_plan_shape(const HostFrame* frames, uint64_t nf, uint32_t k4j_min, PlanShape* out, hipStream_t s) {
@@ -4868,10 +4871,10 @@ hipError_t launch_plan_shape(const HostFrame* frames, uint64_t nf, uint32_t k4j_
   return hipGetLastError();
 }
 hipError_t launch_plan_count(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
-                             uint64_t* cnt, uint64_t* tot, hipStream_t s) {
+                             uint64_t* cnt, uint64_t* tot, PlanShape* shape, hipStream_t s) {
   const uint32_t nt = (uint32_t)((nf + 255) / 256);
   if (nf) {
-    hipLaunchKernelGGL(zd_k_plan_count, dim3(nt), dim3(256), 0, s, X, frames, blocks, nf, (PlanCounts*)cnt);
+    hipLaunchKernelGGL(zd_k_plan_count, dim3(nt), dim3(256), 0, s, X, frames, blocks, nf, (PlanCounts*)cnt, shape);
     hipLaunchKernelGGL(zd_k_plan_scan_tiles, dim3(nt), dim3(256), 0, s, cnt, nf, tot);
   }
   hipLaunchKernelGGL(zd_k_plan_scan_sums, dim3(1), dim3(64), 0, s, tot, (uint64_t)nt);

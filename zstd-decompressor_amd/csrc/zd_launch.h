@@ -59,10 +59,10 @@ hipError_t launch_walk(const uint8_t* src, uint64_t n, uint64_t first, uint64_t 
 // zeroed first), the count pass + exclusive scan (cnt: nf x PLAN_FIELDS
 // words, scanned within 256-frame tiles; tot: (tiles + 1) x PLAN_FIELDS
 // words, the tiles' starts and then the plan's totals), the fill pass.
-struct PlanShape { uint32_t multi, jcand; };
+struct PlanShape { uint32_t multi, jcand; uint64_t jmaxseq; };
 hipError_t launch_plan_shape(const HostFrame* frames, uint64_t nf, uint32_t k4j_min, PlanShape* out, hipStream_t s);
 hipError_t launch_plan_count(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
-                             uint64_t* cnt, uint64_t* tot, hipStream_t s);
+                             uint64_t* cnt, uint64_t* tot, PlanShape* shape, hipStream_t s);
 hipError_t launch_plan_fill(const PlanCtx& X, const HostFrame* frames, const HostBlock* blocks, uint64_t nf,
                             const uint64_t* cnt, const uint64_t* tot, const Sink& S, hipStream_t s);
 

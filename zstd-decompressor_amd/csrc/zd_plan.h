@@ -40,14 +40,17 @@ struct PlanCounts {
   uint64_t tables = 0, huf = 0, seq = 0, k4f = 0, copies = 0;
   uint64_t jframes = 0, jblk = 0, jseg = 0;
   uint64_t inexact = 0;          // frames whose capacity is an upper bound (no usable FCS)
+  uint64_t jwords = 0;           // K4J state words: a frame's region starts a 16-word piece, 16 words of slack after
+  uint64_t jpieces = 0;          // K4J 16-byte pieces over the frames' regions
   ZD_HD bool exact() const { return inexact == 0; }
   ZD_HD void add(const PlanCounts& o) {
     frames += o.frames; blocks += o.blocks; comps += o.comps; luts += o.luts; fses += o.fses; lits += o.lits;
     nrec += o.nrec; nseq += o.nseq; out += o.out; tables += o.tables; huf += o.huf; seq += o.seq; k4f += o.k4f;
     copies += o.copies; jframes += o.jframes; jblk += o.jblk; jseg += o.jseg; inexact += o.inexact;
+    jwords += o.jwords; jpieces += o.jpieces;
   }
 };
-constexpr int PLAN_FIELDS = 18;
+constexpr int PLAN_FIELDS = 20;
 static_assert(sizeof(PlanCounts) == PLAN_FIELDS * 8, "PlanCounts: u64 fields only");
 
 // Plan-wide inputs of the per-frame pass.  `prev_*` seed the Treeless/Repeat
@@ -82,10 +85,13 @@ struct Sink {
 
 // One frame's descriptors at the running indices c (build_plan).  FILL: the
 // entries are written to S; otherwise c only advances (the counting pass).
-// Frames for K4J are listed in *jfr (their descriptors come after, in order).
+// A K4J frame's descriptors (JFrame, its JBlkDesc and JSegDesc entries) are
+// written here too, at the running K4J indices, so the host and the device
+// build them alike; jm->note(n) gets each K4J frame's sequence count (the
+// plan's pointer-jumping rounds follow the largest).
 template <bool FILL, typename JOUT>
 ZD_HD void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hblocks, PlanCounts& c, const Sink& S,
-                      JOUT* jfr) {
+                      JOUT* jm) {
   const uint32_t fi = (uint32_t)c.frames;
   FrameDesc fd{};
   FrameState fs{};
@@ -218,10 +224,38 @@ ZD_HD void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hb
     fs.key = plan_min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
   if (to_j) {
     fd.lds = 2;
+    uint64_t nseq = 0;
+    uint32_t njs = (uint32_t)c.jseg;
+    for (uint32_t k = 0; k < fd.nblocks; k++) {
+      const HostBlock& hb = hblocks[hf.b0 + k];
+      const uint32_t bn = hb.type == 2 ? hb.cb.nseq : 0u;
+      nseq += bn;
+      if (FILL) {
+        JBlkDesc d{};
+        d.block = fd.first_block + k;
+        d.jframe = (uint32_t)c.jframes;
+        d.j = k;
+        d.seg0 = njs;
+        for (uint32_t g = 0; g == 0 || g * J_SEG < bn; g++) S.jsegd[njs++] = JSegDesc{(uint32_t)c.jblk + k, g};
+        S.jblkd[c.jblk + k] = d;
+      }
+    }
+    if (FILL) {
+      JFrame jf{};
+      jf.base = c.jwords;                      // word index: frame pieces of 16 words are 64-byte lines
+      jf.cap = cap;
+      jf.piece0 = c.jpieces;
+      jf.frame = fi;
+      jf.jb0 = (uint32_t)c.jblk;
+      jf.njb = fd.nblocks;
+      S.jframes[c.jframes] = jf;
+    }
+    if (jm) jm->note(nseq);
     c.jframes++;
     c.jblk += fd.nblocks;
     c.jseg += jseg;
-    if (FILL) jfr->push_back(fi);
+    c.jwords += plan_align(cap + 16, 16);
+    c.jpieces += (cap + 15) / 16;
   } else {
     // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
     // executes the frames that fit it in plans of 256-768 frames, where the

@@ -87,6 +87,8 @@ SIGNATURES = {
     "zd_shard_partition": (C.c_int, [C.POINTER(C.c_uint64), _sz, C.c_int, _szp]),
     "zd_shard_range": (C.c_int, [_vp, _sz, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                  C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "zd_plan_frame_outputs": (C.c_int, [_vp, C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                        C.c_size_t, C.POINTER(C.c_size_t)]),
     "zd_comm_unique_id": (C.c_int, [_vp]),
     "zd_comm_create": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_vp)]),
     "zd_comm_destroy": (None, [_vp]),

@@ -10,6 +10,14 @@ Frame.parse as in the reference, whatever block it is in; the frame's output
 or its execution error (phase 1) is kept for decode() (ZStandard::decode,
 frame.rs:232-260).  Host-only callers that want the index without a GPU
 pass use zd_frames_index (batch.frames_index).
+
+FrameIterator (frame.rs:86-99, the loop of src/main.rs:43-53) does not pay a
+plan + launch + sync per frame: it decodes the parser's remaining bytes in
+ONE zd_plan_decompress and hands out each frame's status and bytes from it
+(zd_plan_frame_outputs), with the same per-frame parse / decode errors as
+Frame.parse.  Frames after the batch's first failing frame were not decoded
+(ZD_E_NOT_DECODED): an iterator that goes on past a failure decodes the rest
+in a new batch from there.
 """
 from __future__ import annotations
 
@@ -108,9 +116,86 @@ class Frame:
         return self.inner.decode()
 
 
+class _Batch:
+    """One GPU decode of a parser's remaining bytes, frame by frame: the host
+    index of the frames (zd_frames_index), one zd_plan_decompress, and each
+    frame's (status, offset, length) in the output (zd_plan_frame_outputs)."""
+
+    def __init__(self, data: bytes, start: int):
+        from .batch import Plan, KEY_NONE
+        L = _lib.lib()
+        self.start, self.data = start, data
+        p, n, keep = _lib.buf(data)
+        nf, nb, cons = C.c_size_t(), C.c_size_t(), C.c_size_t()
+        L.zd_frames_index(p, n, None, 0, C.byref(nf), None, 0, C.byref(nb), C.byref(cons))
+        self.fa = (FrameDesc * max(nf.value, 1))()
+        self.ba = (BlockDesc * max(nb.value, 1))()
+        L.zd_frames_index(p, n, self.fa, nf.value, C.byref(nf), self.ba, nb.value, C.byref(nb), C.byref(cons))
+        self.nf = nf.value
+        self.key = KEY_NONE
+        self.first = -1                      # the batch's first failing frame (its key is the plan's)
+        self.status = [0] * self.nf
+        self.off = [0] * self.nf
+        self.len = [0] * self.nf
+        self.out = b""
+        self.next = 0                        # the next frame to hand out
+        if self.nf == 0:
+            return
+        plan = Plan(data)
+        try:
+            cap = max(plan.info.out_bytes, 1)
+            for _ in range(2):
+                out = (C.c_uint8 * cap)()
+                ol = C.c_size_t()
+                st = L.zd_plan_decompress(plan._h, p, n, out, cap, C.byref(ol))
+                if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
+                    _lib.check(st, "zd_plan_decompress")
+                if ol.value <= cap:
+                    break
+                cap = ol.value
+            self.out = bytes(out[: min(ol.value, cap)])
+            self.key = plan.refresh_info().error_key
+            fs = (C.c_int32 * self.nf)()
+            fo = (C.c_uint64 * self.nf)()
+            fl = (C.c_uint64 * self.nf)()
+            m = C.c_size_t()
+            _lib.check(L.zd_plan_frame_outputs(plan._h, fs, fo, fl, self.nf, C.byref(m)), "zd_plan_frame_outputs")
+            k = min(m.value, self.nf)
+            self.status[:k], self.off[:k], self.len[:k] = list(fs)[:k], list(fo)[:k], list(fl)[:k]
+            for f in range(k, self.nf):
+                self.status[f] = _lib.NOT_DECODED
+            self.first = next((f for f in range(self.nf) if self.status[f] != 0), -1)
+        finally:
+            plan.close()
+
+    def frame(self, parser):
+        """Frame.parse for the parser's next frame from this batch, or None
+        when the batch does not hold it (past a failure, or not indexed)."""
+        f = self.next
+        if parser._pos != self.start + (self.fa[f].src_offset if f < self.nf else -1) or f >= self.nf:
+            return None
+        st = self.status[f]
+        if st == _lib.NOT_DECODED:
+            return None
+        from .batch import PH_PARSE, KEY_NONE
+        d = self.fa[f]
+        raw = self.data[d.src_offset:d.src_offset + d.src_size]
+        self.next += 1
+        parser.advance(d.src_size)
+        if d.kind == 1:
+            return Frame(Skippable(d.magic, raw[8:]))
+        from .block import Block
+        blocks = [Block._from_desc(raw, self.ba[d.first_block + i], d.src_offset) for i in range(d.num_blocks)]
+        if st != 0 and f == self.first and self.key != KEY_NONE and (self.key >> 62) == PH_PARSE:
+            raise ZdError(st, "Frame::parse")        # a Huffman / FSE table description (ZStandard::parse)
+        out = self.out[self.off[f]:self.off[f] + self.len[f]] if st == 0 else b""
+        return Frame(ZStandard(raw, d, blocks, (st, out)))
+
+
 class FrameIterator:              # frame.rs:86-99
     def __init__(self, parser):
         self.parser = parser
+        self._batch = None
 
     def __iter__(self):
         return self
@@ -118,4 +203,11 @@ class FrameIterator:              # frame.rs:86-99
     def __next__(self) -> Frame:
         if self.parser.is_empty():
             raise StopIteration
-        return Frame.parse(self.parser)
+        fr = self._batch.frame(self.parser) if self._batch is not None else None
+        if fr is None:
+            # a new batch from here (the first call, or past the last batch's failure)
+            self._batch = _Batch(self.parser.remaining(), self.parser._pos)
+            fr = self._batch.frame(self.parser)
+        if fr is None:                          # a frame the host index rejects: Frame.parse raises its error
+            return Frame.parse(self.parser)
+        return fr
