@@ -297,6 +297,9 @@ def main():
     ap.add_argument("--share", default=None, metavar="R/N",
                     help="one GPU, one process: decode only rank R's frame range of the N-way strong partition "
                          "(the share one rank of an N-GPU run decodes, measured alone; no gather)")
+    ap.add_argument("--overlap-streams", type=int, default=0, metavar="N",
+                    help="also time the corpus as N contiguous frame chunks, each its own plan on its own stream "
+                         "(K1/K2 of one chunk beside K3/K4 of another; reported apart, never value)")
     ap.add_argument("--experiment", action="store_true",
                     help="timing-only variants: do not stop on decode errors")
     args = ap.parse_args()
@@ -472,6 +475,53 @@ def main():
     plan.set_profiling(False)
     kt = {k: float(np.mean(v)) for k, v in kt.items()}
 
+    # ---- chunks on parallel streams (an experiment: reported apart) ----
+    overlap = None
+    if args.overlap_streams > 1 and world == 1:
+        N = args.overlap_streams
+        fr = frames_index(data)[0]
+        cut = [len(fr) * k // N for k in range(N + 1)]
+        subs, ob = [], 0
+        for k in range(N):
+            a = fr[cut[k]]["src_offset"]
+            b = fr[cut[k + 1] - 1]["src_offset"] + fr[cut[k + 1] - 1]["src_size"]
+            sp = Plan(data[a:b])
+            subs.append((sp, a, ob, torch.cuda.Stream(dev)))
+            ob += int(sp.info.out_bytes)
+        assert ob == info.out_bytes
+
+        def ostep():
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            for sp, a, o, st_ in subs:
+                st_.wait_event(ev)
+                sp.decode_async(d_src.data_ptr() + a, d_dst.data_ptr() + o, int(sp.info.out_bytes), st_.cuda_stream)
+            for sp, a, o, st_ in subs:
+                e2 = torch.cuda.Event()
+                e2.record(st_)
+                stream.wait_event(e2)
+        for _ in range(2):
+            ostep()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            ostep()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        oms = e0.elapsed_time(e1) / args.steps
+        ook = None
+        if src is not None and not args.no_verify:
+            ook = all(sp.results(d_dst.data_ptr() + o, st_.cuda_stream)[0] == 0 for sp, a, o, st_ in subs)
+            ref = torch.frombuffer(bytearray(src), dtype=torch.uint8).to(dev)
+            u = len(src)
+            ook = ook and all(bool(torch.equal(d_dst[r * u:(r + 1) * u], ref)) for r in range(reps))
+            del ref
+        overlap = {"chunks": N, "ms_per_step": round(oms, 3), "MBps": round(info.out_bytes / (oms / 1e3) / 1e6, 1),
+                   "vs_one_plan_ms": round(ms_per_step, 3), "verified_bit_exact": ook}
+        for sp, a, o, st_ in subs:
+            sp.close()
+
     # ---- gather of the decoded ranges to rank 0 over RCCL (never part of value) ----
     out_bytes = info.out_bytes
     comp_bytes = len(data)
@@ -624,6 +674,8 @@ def main():
         }
         if gather:
             res["gather_to_rank0"] = gather
+        if overlap:
+            res["overlap_streams"] = overlap
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -26,7 +26,8 @@ def _outcomes(data, batched):
             res.append((e.code, None, b""))
             break                                   # the frame could not be parsed: nothing follows it
         try:
-            res.append((None, None, f.decode()))
+            # (a skippable frame's payload is not part of the CLI's output without -p)
+            res.append((None, None, b"" if f.is_skippable else f.decode()))
         except ZdError as e:
             res.append((None, e.code, b""))
     return res
@@ -54,11 +55,13 @@ def test_frame_iterator_matches_frame_parse():
     for name, data in _cases().items():
         a = _outcomes(data, True)
         b = _outcomes(data, False)
-        assert a == b, name
+        same = a == b                                   # (no pytest diff of megabytes of bytes)
+        assert same, (name, [(x[0], x[1], len(x[2])) for x in a], [(x[0], x[1], len(x[2])) for x in b])
         # and the frames that decoded are the reference's bytes
         good = b"".join(x[2] for x in a if x[0] is None and x[1] is None)
         if all(x[0] is None and x[1] is None for x in a):
-            assert good == oracle.decompress(data), name
+            ok = good == oracle.decompress(data)
+            assert ok, name
 
 
 @pytest.mark.gpu
@@ -78,5 +81,6 @@ def test_frame_iterator_is_one_decode_per_batch():
         out = b"".join(f.decode() for f in ForwardByteParser(data).iter())
     finally:
         fr._Batch.__init__ = orig
-    assert out == oracle.decompress(data)
+    ok = out == oracle.decompress(data)
+    assert ok
     assert len(made) == 1
