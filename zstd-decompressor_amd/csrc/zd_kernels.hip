@@ -2323,7 +2323,7 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 #define ZD_K4_INWIN 1
 #endif
 #ifndef ZD_K4_OVS
-#define ZD_K4_OVS 0                         // pass 0: merged 16-byte chunks written past their end
+#define ZD_K4_OVS 1                         // pass 0: merged 16-byte chunks written past their end (0: exact per-part stores)
 #endif
 constexpr int K4_WPAD = ZD_K4_OVS ? 16 : 0;  // LDS bytes below the window
 #ifndef ZD_K4_STG
