@@ -52,6 +52,7 @@ for s in "$@"; do
     profc2big) run prof_c2_1GiB 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2big -o run --output-format csv -- python bench.py --workload c2 --c2-mib 1024 --steps 3 --warmup 1 --no-cpu-baseline --no-host-io ;;
     share:*) x=${s#share:}; run bench_share_${x//\//of} 600 python bench.py --share $x --no-cpu-baseline --no-host-io ;;
     testvar:*) v=${s#testvar:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run pytest_var_$v 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    k3g:*) v=${s#k3g:}; ZD_K3G=$v run bench_k3g_$v 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     ovlp:*) n=${s#ovlp:}; run bench_ovlp_$n 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io --overlap-streams $n ;;
     titer) run pytest_iter 300 python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu tests/test_frame_iterator.py tests/test_lds_order.py ;;
     ldsorder) run lds_order 120 tools/lds_order_check 4096 256 ;;
