@@ -439,9 +439,6 @@ struct JSegDesc {          // static: the scatter's work list
   uint32_t k;              // segment of the block
 };
 
-// K3G's per-chain table slot in HBM: OF 256 | ML 512 | LL 512 | LL 512 u16 (zd_kernels.hip zd_k_sequences_g)
-constexpr uint64_t K3G_SLOT_BYTES = 2 * (256 + 512 + 512 + 512);
-
 // Workspace carve-up, all offsets in bytes from the workspace base.
 struct Workspace {
   uint64_t comp, comp_state, blocks, frames, frame_state, frame_state0;
@@ -454,7 +451,6 @@ struct Workspace {
   uint64_t jst;                                         // K4J per-byte state words
   uint64_t redo, k2done;                                // zd_k_fused: frames for the redo pass, K2's finished workgroups
   uint64_t hframes;                                     // device-built plans: the walk's frame index (zd_walk.h HostFrame)
-  uint64_t k3g;                                         // K3G: per-chain table slots (K3G_SLOT_BYTES each)
   uint64_t total;
 };
 

@@ -206,12 +206,10 @@ Route route_plan(const RouteIn& in) {
 // The environment overrides (experiments only), read once
 struct RouteEnv {
   int fuse = -1, k4f = -1, fork = -1, k1fork = -1;
-  int k3g = -1;                      // percent of the sequence blocks on K3G (experiments)
   int64_t k1w_max = -1;
   RouteEnv() {
     auto get = [](const char* n) { const char* e = getenv(n); return e ? atoi(e) : -1; };
     fuse = get("ZD_FUSE"); k4f = get("ZD_K4F"); fork = get("ZD_FORK"); k1fork = get("ZD_K1FORK");
-    k3g = get("ZD_K3G");
     if (const char* e = getenv("ZD_K1W_MAX")) k1w_max = atoll(e);
   }
 };
@@ -434,7 +432,6 @@ void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint
   W.jst = carve(4 * P->j_bytes + 64);
   W.redo = carve(std::max<uint64_t>(T.frames, 1));
   W.k2done = carve(4);
-  W.k3g = carve(K3G_SLOT_BYTES * std::max<uint64_t>(T.seq, 1));
 }
 // The plan's array counts from the totals
 void plan_totals(zd_plan* P, const PlanCounts& T, bool fused) {
@@ -1636,11 +1633,6 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
     a.k1_fork = true;
   }
   a.k1_seq_waves = E.k1w_max >= 0 ? P->n_tables <= (uint64_t)E.k1w_max && !(P->flags & ZD_F_K1_LANES) : r.k1_seq_waves;
-  // K3G beside K3Q (the tail of the sequence list), when neither fork uses the second stream
-  if (!fork && E.k3g > 0 && !P->profile && a.k3_quad && !P->fused) {
-    a.k3g_n = (uint32_t)(P->n_seq * (uint64_t)std::min(E.k3g, 100) / 100);
-    if (a.k3g_n) { a.aux = P->aux; a.fork = P->fork; a.join = P->join; }
-  }
   P->last_fused = P->fused && !P->profile;
   if (P->last_fused) {
     a.fused = true;

@@ -1840,8 +1840,8 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
-template <int L, int N, bool PUB = false, typename TP = const lds_u16*>
-__device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, TP tab, int role,
+template <int L, int N, bool PUB = false>
+__device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
                           volatile __attribute__((address_space(3))) uint32_t* prog = nullptr) {
   constexpr int U = (L % 2 == 0) ? L : 2 * L;
@@ -2029,77 +2029,6 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
     exact = seq_chainq<ZD_K3_LA, ZD_K3_WN>(blk + cs.bs_off, cs.bs_size, lo, tab, role, al[0], al[1], al[2], C.nseq,
                                           recs + C.seq_out) != 0;
   }
-  if (exact && role == 0)
-    st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0],
-                                 al[1], al[2], C.nseq, recs + C.seq_out);
-  if (st) k3_fail(C, ci, cstate, fstate, st);
-}
-// K3G: the K3Q chains with their tables in HBM instead of LDS (a per-chain
-// scratch slot, K3G_TAB u16 entries: each lane's own table, written and read
-// by that lane only, so no cross-lane visibility is needed).  No LDS, so its
-// waves run beside the LDS-bound K3Q waves on the SIMDs' idle issue slots
-// (one K3Q wave per SIMD leaves ~half of the VALU cycles unused); the plan's
-// sequence list is split between the two launches (zd_host.cpp k3g_split).
-constexpr int K3G_TAB = 256 + 512 + 512 + 512;      // OF | ML | LL | LL again (the shadow lane's)
-__global__ __launch_bounds__(64) void zd_k_sequences_g(const uint8_t* __restrict__ src,
-                                                       const CompBlock* __restrict__ comp, CompState* cstate,
-                                                       FrameState* fstate, const uint32_t* __restrict__ list,
-                                                       uint32_t n_list, const uint16_t* __restrict__ fses,
-                                                       uint64_t* __restrict__ recs, uint16_t* __restrict__ k3g) {
-  const int lane = threadIdx.x;
-  const int role = lane & 3, q = lane >> 2;
-  const uint32_t li = blockIdx.x * K3Q_CHAINS + q;
-  bool act = q < K3Q_CHAINS && li < n_list;
-  const uint32_t ci = act ? list[li] : 0;
-  CompBlock C;
-  if (act) C = comp[ci];
-  if (act) {
-    const uint64_t key0 = fstate[C.frame].key;
-    if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) act = false;
-  }
-  if (!act) return;
-  int al[3];
-  const uint16_t* g[3];
-  for (int k = 0; k < 3; k++) {
-    const uint32_t sidx = (uint32_t)C.tab_src[k];
-    al[k] = cstate[sidx].al[k];
-    g[k] = fses + (uint64_t)comp[sidx].fse_slot * FSE_SLOT + k * FSE_TAB;
-  }
-  const bool use_tab = al[1] <= 8;                  // (as K3Q: an OF table of 512 states takes the exact chain)
-  // role -> fses table k (0 LL, 1 OF, 2 ML) and its region in the slot
-  const int k = role == 0 ? 1 : role == 1 ? 2 : 0;
-  const int at = role == 0 ? 0 : role == 1 ? 256 : role == 2 ? 768 : 1280;
-  uint16_t* mine = k3g + (uint64_t)li * K3G_TAB + at;
-  if (use_tab) {
-    const int cnt = 1 << al[k];
-    if (cnt >= 8) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      typedef __attribute__((address_space(1))) const u32x4 g_u4;
-      typedef __attribute__((address_space(1))) u32x4 gw_u4;
-      g_u4* s4 = (g_u4*)g[k];
-      gw_u4* d4 = (gw_u4*)mine;
-      for (int e = 0; e < cnt / 8; e++) {
-        u32x4 v = s4[e];
-        v.x = K3_ENTRY(v.x & 0xFFFF, k, al[k]) | (K3_ENTRY(v.x >> 16, k, al[k]) << 16);
-        v.y = K3_ENTRY(v.y & 0xFFFF, k, al[k]) | (K3_ENTRY(v.y >> 16, k, al[k]) << 16);
-        v.z = K3_ENTRY(v.z & 0xFFFF, k, al[k]) | (K3_ENTRY(v.z >> 16, k, al[k]) << 16);
-        v.w = K3_ENTRY(v.w & 0xFFFF, k, al[k]) | (K3_ENTRY(v.w >> 16, k, al[k]) << 16);
-        d4[e] = v;
-      }
-    } else {
-      for (int e = 0; e < cnt; e++) mine[e] = (uint16_t)K3_ENTRY(((g_u16*)g[k])[e], k, al[k]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the lane's own stores, before its loads
-  }
-  const CompState cs = cstate[ci];
-  const uint8_t* blk = src + C.src;
-  const uintptr_t lo = (uintptr_t)src;
-  int st = 0;
-  bool exact = !use_tab;
-  if (use_tab)
-    exact = seq_chainq<ZD_K3_LA, ZD_K3_WN, false, g_u16*>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)mine, role, al[0],
-                                                          al[1], al[2], C.nseq, recs + C.seq_out) != 0;
-  // (the quad's lanes agree: the chain's verdict is quad-uniform)
   if (exact && role == 0)
     st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, lo, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0],
                                  al[1], al[2], C.nseq, recs + C.seq_out);
@@ -4524,7 +4453,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   // K2 and K3 are independent once their tables exist: with the fork, K1's
   // Huffman half and K2 run on the aux stream beside K1's sequence half and
   // K3 (not when timing kernels one by one)
-  const bool fork = a.aux && !a.k1_fork && !a.k3g_n && !a.events && a.n_huf && a.n_seq;
+  const bool fork = a.aux && !a.k1_fork && !a.events && a.n_huf && a.n_seq;
   // without it, K1's two halves may still run on the two streams (joined
   // before K2)
   const bool k1f = a.aux && a.k1_fork && !a.events && a.n_tables;
@@ -4580,17 +4509,6 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   auto k3 = [&](const uint32_t* list, uint32_t n, hipStream_t st, const uint8_t* redo) {
-    if (n && a.k3g_n && !redo && !a.events && a.k3g_n <= n) {
-      // the list's tail on K3G on the second stream, beside K3Q (joined before K4)
-      const uint32_t nq = n - a.k3g_n;
-      (void)hipEventRecord(a.fork, st);
-      (void)hipStreamWaitEvent(a.aux, a.fork, 0);
-      hipLaunchKernelGGL(zd_k_sequences_g, dim3((a.k3g_n + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, a.aux, a.src,
-                         comp, cstate, fstate, list + nq, a.k3g_n, (const uint16_t*)fses, seqs,
-                         (uint16_t*)(ws + W.k3g));
-      (void)hipEventRecord(a.join, a.aux);
-      n = nq;
-    }
     if (n) {
       if (a.k3_quad)
         hipLaunchKernelGGL(zd_k_sequences_q, dim3((n + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, st, a.src, comp,
@@ -4642,7 +4560,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     if ((e = k4(0, a.n_frames, s, redo)) != hipSuccess) return e;
   } else {
     k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, nullptr);
-    if (fork || (a.k3g_n && !a.events))
+    if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
     if ((e = k4(0, a.n_frames, s, nullptr)) != hipSuccess) return e;

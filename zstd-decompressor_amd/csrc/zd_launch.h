@@ -27,7 +27,6 @@ struct LaunchArgs {
   bool fused = false;                      // K3 + K4 as zd_k_fused, then the redo pass
   bool k1_seq_waves = false;               // K1's sequence half one wave per block (zd_k_tables_seqw)
   bool k1_fork = false;                    // no K2 | K3 fork: K1's halves on the two streams (aux, fork, join)
-  uint32_t k3g_n = 0;                      // the last k3g_n sequence blocks on K3G (aux stream, beside K3Q)
   // optional (zd_plan_set_profiling mode 2): an event pair recorded on
   // `stream` around each launch group that can carry a plan's work -- K0,
   // zd_k_fused, K4, K4F, the K4J kernels (kDomNames) -- with the fork and
