@@ -1843,9 +1843,6 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 #ifndef ZD_K3_DPPASM
 #define ZD_K3_DPPASM 1
 #endif
-#ifndef ZD_K3_WIN1
-#define ZD_K3_WIN1 1
-#endif
 template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
@@ -1908,17 +1905,8 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     const int32_t y = (pos - use.wb) - (int32_t)csum;
     pos -= (int32_t)csum;
     ymin = min(ymin, y);
-#if ZD_K3_WIN1
-    // the quad's OF lane alone loads the windows (a quarter of the lanes
-    // through the texture path: the four lanes' windows were the same) and
-    // its 32 bits at y go to the quad with one DPP broadcast; the other
-    // lanes' window registers and y are stale and unused
-    const uint32_t r = qdpp<0x00>(winn_at_tree<N>(use, (uint32_t)y));
-    if (role == 0) use = winn_load<N>(bs, m, pos);
-#else
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
     use = winn_load<N>(bs, m, pos);
-#endif
     // the state bits sit OF | ML | LL upwards from y: offsets 0, nbO, nbO +
     // nbM (the shadow takes the LL lane's), by quad_perm [0,0,1,1] twice
 #if ZD_K3_DPPASM
