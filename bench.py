@@ -665,6 +665,10 @@ def main():
             "host_plan_split_ms": {"headers_and_descriptors": round(info.host_ns / 1e6, 1),
                                    "workspace_alloc_and_upload": round(info.device_ns / 1e6, 1)},
             "value_incl_host_plan": round(total_out.item() / (ms_per_step / 1e3 + host_plan_s) / 1e6, 1),
+            # the same with the plan built on the GPU from the HBM-resident input
+            # (zd_plan_create_device: header walk + descriptors), one plan per step
+            "value_incl_device_plan": None if dev_plan_ms is None else
+            round(total_out.item() / (ms_per_step / 1e3 + dev_plan_ms / 1e3) / 1e6, 1),
             "h2d_ms": None if not host_io else host_io["h2d_ms"],
             "d2h_ms": None if not host_io else host_io["d2h_ms"],
             "host_io": host_io,

@@ -53,6 +53,7 @@ for s in "$@"; do
     share:*) x=${s#share:}; run bench_share_${x//\//of} 600 python bench.py --share $x --no-cpu-baseline --no-host-io ;;
     testvar:*) v=${s#testvar:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run pytest_var_$v 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     k3g:*) v=${s#k3g:}; ZD_K3G=$v run bench_k3g_$v 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
+    c5var:*) v=${s#c5var:}; l=${v#*@}; v=${v%@*}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c5var_${v}_L$l 900 python bench.py --workload c5 --level $l --no-cpu-baseline --no-host-io ;;
     ovlp:*) n=${s#ovlp:}; run bench_ovlp_$n 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io --overlap-streams $n ;;
     titer) run pytest_iter 300 python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu tests/test_frame_iterator.py tests/test_lds_order.py ;;
     ldsorder) run lds_order 120 tools/lds_order_check 4096 256 ;;

@@ -2341,6 +2341,10 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 #define ZD_K4_OVS 1                         // pass 0: merged 16-byte chunks written past their end (0: exact per-part stores)
 #endif
 constexpr int K4_WPAD = ZD_K4_OVS ? 16 : 0;  // LDS bytes below the window
+#ifndef ZD_K4_OVS_TRIP
+#define ZD_K4_OVS_TRIP 2                    // pass 0: chunks past the second, this many per trip, loads first
+#endif
+constexpr uint32_t K4_OVS_TRIP = ZD_K4_OVS_TRIP;
 #ifndef ZD_K4_STG
 #define ZD_K4_STG 512                       // C4, 4 GiB: 1024 8.36 ms, 512 8.25, 256 8.24
 #endif
@@ -2773,18 +2777,15 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
           const uint32_t last = n0 >= 16 ? n0 - 16 : 0u;
           const bool src_far = full0 && far0;
           const bool src_win = full0 && inwin;
-          for (uint32_t b0 = 0, it = 0;; b0 += 16, it++) {
-            const uint32_t bb = min(b0, last);
-            const uint32_t kl = ll > bb ? min(ll - bb, 16u) : 0u;      // literal bytes in the chunk
+          // the chunk at byte bb of the lane's run: ll - bb literal bytes from
+          // the stage, then match bytes mv (read at msrc(bb))
+          auto msrc = [&](uint32_t bb) -> int32_t {
+            return ll >= bb + 16 ? slo : slo + (int32_t)bb - (int32_t)ll;
+          };
+          auto put = [&](uint32_t bb, u32x4 mv) {
+            const uint32_t kl = ll > bb ? min(ll - bb, 16u) : 0u;   // literal bytes in the chunk
             u32x4 lv = f4;
             if (lit_stage) lv = lds16((const l_u8*)stg + min(lpos + bb, K4_STG));
-            u32x4 mv = lv;
-            if (kl < 16) {
-              const int32_t ma = slo + (int32_t)bb - (int32_t)ll;
-              if (src_far) mv = it == 0 ? fv0 : it == 1 ? fv1 : ldg16_src(X.out + (uint32_t)ma);
-              else if (src_win) mv = lds16(X.at(ma));
-            }
-            // bytes [0, kl) from lv, the rest from mv
             const uint64_t mlo = kl >= 8 ? ~0ull : ((1ull << (8 * kl)) - 1);
             const uint64_t mhi = kl >= 16 ? ~0ull : (kl <= 8 ? 0ull : ((1ull << (8 * (kl - 8))) - 1));
             u32x4 v;
@@ -2793,7 +2794,22 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
             v.z = ((uint32_t)mhi & lv.z) | (~(uint32_t)mhi & mv.z);
             v.w = ((uint32_t)(mhi >> 32) & lv.w) | (~(uint32_t)(mhi >> 32) & mv.w);
             *(l_u32x4a1*)(d + bb) = v;
-            if (b0 + 16 >= n0) break;
+          };
+          auto mload = [&](uint32_t bb) -> u32x4 {
+            return src_far ? ldg16_src(X.out + (uint32_t)msrc(bb)) : src_win ? lds16(X.at(msrc(bb))) : f4;
+          };
+          // chunks 0 and 1 (a far lane's match bytes were loaded above), then
+          // four at a time, their loads first (no match here overlaps itself)
+          put(0, src_far ? fv0 : mload(0));
+          if (n0 > 16) put(min(16u, last), src_far ? fv1 : mload(min(16u, last)));   // (far: bb1 == min(16, last))
+          for (uint32_t j0 = 2; 16 * j0 < n0; j0 += K4_OVS_TRIP) {
+            u32x4 m[K4_OVS_TRIP];
+#pragma unroll
+            for (uint32_t q = 0; q < K4_OVS_TRIP; q++)
+              if (16 * (j0 + q) < n0) m[q] = mload(min(16 * (j0 + q), last));
+#pragma unroll
+            for (uint32_t q = 0; q < K4_OVS_TRIP; q++)
+              if (16 * (j0 + q) < n0) put(min(16 * (j0 + q), last), m[q]);
           }
         }
         if (__ballot(lslow)) {                         // literals past the stage: exact, from HBM
