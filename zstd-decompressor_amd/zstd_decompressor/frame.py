@@ -122,7 +122,7 @@ class _Batch:
     frame's (status, offset, length) in the output (zd_plan_frame_outputs)."""
 
     def __init__(self, data: bytes, start: int):
-        from .batch import Plan, KEY_NONE
+        from .batch import Plan, KEY_NONE, run_plan
         L = _lib.lib()
         self.start, self.data = start, data
         p, n, keep = _lib.buf(data)
@@ -143,17 +143,7 @@ class _Batch:
             return
         plan = Plan(data)
         try:
-            cap = max(plan.info.out_bytes, 1)
-            for _ in range(2):
-                out = (C.c_uint8 * cap)()
-                ol = C.c_size_t()
-                st = L.zd_plan_decompress(plan._h, p, n, out, cap, C.byref(ol))
-                if st in (_lib.HIP, _lib.INVALID_ARG, _lib.NO_MEMORY):
-                    _lib.check(st, "zd_plan_decompress")
-                if ol.value <= cap:
-                    break
-                cap = ol.value
-            self.out = bytes(out[: min(ol.value, cap)])
+            st, self.out = run_plan(plan, p, n)
             self.key = plan.refresh_info().error_key
             fs = (C.c_int32 * self.nf)()
             fo = (C.c_uint64 * self.nf)()
