@@ -118,3 +118,32 @@ def test_single_frame_over_128MiB():
     assert oracle.decompress(data) == src
     assert _gpu(data) == (0, src)
     assert _gpu(data, fs) == (0, src)
+
+
+def test_single_frame_over_2GiB():
+    """A single libzstd frame of 2.25 GiB (18,432 blocks): K4J's state words
+    are distances, so frame positions past 2^31 decode (the streaming
+    executor's int32 positions do not reach: forced onto it, the frame is out
+    of the GPU path's domain).  The source is a 256 KiB text tile repeated
+    with a counter stamped into each copy, so every tile copies the one
+    before it: pointer chains as long as the frame has tiles, resolved by the
+    rounds' doubling.  Checked against the source bytes (the oracle would
+    take minutes at this size; the round trip is the property)."""
+    import numpy as np
+    _, fs = _flags()
+    tile = np.frombuffer(gen.text(256 << 10, seed=10), dtype=np.uint8)
+    n = 9 * (1 << 30) // (4 * len(tile))             # 2.25 GiB
+    arr = np.tile(tile, n).reshape(n, len(tile))
+    arr[:, :4] = np.arange(n, dtype="<u4").view(np.uint8).reshape(n, 4)
+    src = arr.tobytes()
+    del arr
+    assert len(src) == (1 << 31) + (1 << 28)
+    data = libzstd.compress(src, 1)
+    from zstd_decompressor.batch import frames_index
+    frames, blocks, st, _ = frames_index(data)
+    assert st == 0 and len(frames) == 1 and len(blocks) >= len(src) // (128 << 10)
+    gst, gout = _gpu(data)                            # automatic: K4J (past the streaming K4's positions)
+    assert gst == 0 and len(gout) == len(src)
+    assert gout == src
+    del gout
+    assert _gpu(data, fs)[0] == OUT_OF_DOMAIN

@@ -138,7 +138,7 @@ constexpr uint32_t DIRECT_GIANT = (1u << 29) - 1;
 // outside the GPU path's domain (ZD_E_OUT_OF_DOMAIN; the reference's own
 // limit is the 8 MiB window).
 constexpr uint64_t K4_MAX_FRAME_OUT = 0x7FFF0000ull;
-constexpr uint64_t K4J_MAX_FRAME_OUT = 0x7FFF0000ull;   // positions below J_FINAL (zd_kernels.hip K4J)
+constexpr uint64_t K4J_MAX_FRAME_OUT = 1ull << 35;   // 32 GiB: 128 GiB of K4J state words
 constexpr uint64_t OFF_HUGE = ~0ull >> 1;        // a giant offset (never <= a decoded length)
 
 ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t ofv) {
@@ -399,9 +399,11 @@ struct FrameState {
 // K4J: frames of many blocks executed block-parallel (zd_kernels.hip K4J).
 // A frame's bytes are laid out as one u32 state word each in its region
 // [base, base + cap) of the state array: J_FINAL | byte for a byte whose
-// value is known, else the frame position the byte copies (a pointer the
-// pointer-jumping rounds follow, in place; every version of a word is true
-// of the byte, so the rounds need no ordering between lanes).
+// value is known, else the distance back to the byte it copies (a pointer
+// the pointer-jumping rounds follow, in place; every version of a word is
+// true of the byte, so the rounds need no ordering between lanes).
+// Distances keep frames past 2 GiB in reach: only a match source 2 GiB or
+// more behind its byte is out of the domain.
 // ---------------------------------------------------------------------------
 constexpr uint32_t J_FINAL = 1u << 31;
 constexpr int J_MAX_ROUNDS = 40;

@@ -1609,6 +1609,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // 10.2 ms, 2 5.2, 4 3.0, 8 2.44, 16 2.67, 32 2.95); ZD_J_HOPS overrides
   static const char* hops_env = getenv("ZD_J_HOPS");
   a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 8u;
+  a.cus = (uint32_t)(k3_slots() / 64);
   a.stream = s;
   // K3 as four lanes per block (K3Q, default): C3 (763 blocks) 2.89 -> 2.31
   // ms, a forked 8,192-block plan 4.24 -> 2.48, full C4 13.88 -> 13.80; the
@@ -1857,8 +1858,11 @@ int zd::decode_resident(zd_plan* P, const uint8_t* src, size_t n, const uint8_t*
     uint32_t flags = cur->flags;
     uint64_t cap0 = 0;
     if (cur->limit_stage == LS_CAPACITY) {
-      if (old_cap >= K4_MAX_FRAME_OUT) break;      // past the streaming executor's positions: out of domain
-      cap0 = std::min<uint64_t>(K4_MAX_FRAME_OUT, std::max<uint64_t>(4 * old_cap, old_cap + (1u << 20)));
+      // past K4J's 32 GiB, or with K4J forced off the streaming K4's int32
+      // positions (plan_frame keys a larger frame out of domain): stop
+      const uint64_t lim = k4j_mode_of(flags) == 0 ? K4_MAX_FRAME_OUT : K4J_MAX_FRAME_OUT;
+      if (old_cap >= lim) break;
+      cap0 = std::min<uint64_t>(lim, std::max<uint64_t>(4 * old_cap, old_cap + (1u << 20)));
     } else {
       flags = (flags & ~ZD_F_BLOCK_PARALLEL) | ZD_F_FRAME_SERIAL;
       cap0 = old_cap;

@@ -2489,7 +2489,9 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
 
   for (uint32_t j = F.skip; j < F.nblocks && err_key == KEY_NONE; j++) {
     const BlockRec B = blocks[F.first_block + j];
-    if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
+    // a decode error found before (K2), or a limit the plan found (a frame
+    // past the int32 positions: block 0), ends the frame at its block
+    if (key0 != KEY_NONE && key_phase(key0) != PH_PARSE && key_block(key0) <= j) break;
     if (B.type == 5) continue;
     if (B.type == 0 || B.type == 4) {
       if (!k4_emit_lits(X, src + B.src, 0, B.size)) err_key = make_key(PH_LIMIT, j, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN);
@@ -3466,7 +3468,9 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 
   for (uint32_t j = 0; j < F.nblocks; j++) {
     const BlockRec B = blocks[F.first_block + j];
-    if (key0 != KEY_NONE && key_phase(key0) == PH_DECODE && key_block(key0) <= j) break;
+    // a decode error found before (K2), or a limit the plan found (a frame
+    // past the int32 positions: block 0), ends the frame at its block
+    if (key0 != KEY_NONE && key_phase(key0) != PH_PARSE && key_block(key0) <= j) break;
     if (B.type == 5) continue;
     if (B.type != 2) {                            // raw / RLE / skippable payload
       if ((uint64_t)pos + B.size > cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN); break; }
@@ -3790,12 +3794,13 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 //   KJ3 zd_k_jscatter one wave per J_SEG sequences: concrete offsets from the
 //                     checkpoint, the reference's checks; every literal byte's
 //                     state word is J_FINAL | byte, every match byte's the
-//                     frame position it copies (q - off + j mod off: within
-//                     the period of an overlapping match, as the reference's
+//                     distance to the byte it copies (off, plus off per period
+//                     passed in an overlapping match: the reference's
 //                     byte-by-byte push)
-//   KJ4 zd_k_jround   pointer jumping, in place: S[p] = S[S[p]] for every
+//   KJ4 zd_k_jround   pointer jumping, in place: S[p] = S[p - S[p]] for every
 //                     pending word, up to 8 hops per word and round (a final
-//                     source hands over its byte, a pending one its pointer).
+//                     source hands over its byte, a pending one adds its
+//                     distance), one word per lane.
 //                     A chain ends at a literal after at most one hop per
 //                     earlier match, and every hop of a round follows pointers
 //                     earlier rounds have already shortened: a 100 MB text
@@ -4118,15 +4123,7 @@ __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__
 }
 
 typedef __attribute__((address_space(1))) u32x4a1 g_u32x4a1;
-// Bytes [0, n) of a 16-byte piece (n <= 16) to p: one 16-byte store for a
-// whole piece, else byte by byte (a partial piece shares its aligned 16
-// bytes with another lane's).
-__device__ inline void j_store16(uint8_t* p, const u32x4& v, uint32_t n) {
-  if (n == 16) { *(g_u32x4a1*)p = v; return; }
-#pragma unroll
-  for (uint32_t b = 0; b < 16; b++)
-    if (b < n) p[b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
-}
+
 // Words [0, n) of 16 state words to p (n <= 16): four 16-byte stores, or one by one.
 __device__ inline void j_store_words(uint32_t* p, const uint32_t w[16], uint32_t n) {
   if (n == 16) {
@@ -4138,17 +4135,9 @@ __device__ inline void j_store_words(uint32_t* p, const uint32_t w[16], uint32_t
   for (uint32_t b = 0; b < 16; b++)
     if (b < n) p[b] = w[b];
 }
-__device__ inline void j_load_words(const uint32_t* p, uint32_t w[16]) {
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const u32x4 t = *(const g_u32x4a1*)(p + 4 * q);
-    w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
-  }
-}
-
 // n literal bytes from s (HBM) or the fill byte at frame position P0: final.
 // 16-byte pieces aligned in the state array's 64-byte lines.
-__device__ void j_fill_lits(uint32_t* st, uint32_t P0, uint32_t n, const uint8_t* s, uint32_t fill, int lane) {
+__device__ void j_fill_lits(uint32_t* st, uint64_t P0, uint32_t n, const uint8_t* s, uint32_t fill, int lane) {
   if (!n) return;
   const uint32_t g = (16 - (P0 & 15)) & 15;
   const uint32_t np = n > g ? 1 + (n - g + 15) / 16 : 1;
@@ -4189,7 +4178,7 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
   const JFrame JF = jframes[D.jframe];
   uint32_t* st = jst + JF.base;
   const BlockRec B = blocks[D.block];
-  uint32_t pos = (uint32_t)jb[e].out_start;
+  uint64_t pos = jb[e].out_start;
   if (B.type != 2) {
     j_fill_lits(st, pos, B.size, B.type == 1 ? nullptr : src + B.src, B.rle, lane);
     return;
@@ -4204,7 +4193,7 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
   const JSeg G = jseg[D.seg0 + SD.k];
   const uint64_t rin[3] = {jb[e].rep_in[0], jb[e].rep_in[1], jb[e].rep_in[2]};
   uint64_t rep[3] = {jr_apply(G.map[0], rin), jr_apply(G.map[1], rin), jr_apply(G.map[2], rin)};
-  pos += (uint32_t)G.out_rel;
+  pos += G.out_rel;
   uint32_t lit_cursor = G.lit_rel;
   const uint32_t n = C.nseq;
   const uint32_t sb = SD.k * J_SEG, se = min(n, sb + J_SEG);
@@ -4228,11 +4217,18 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
       const bool dbad = valid && lane == bl;
       const bool imp = valid && !dbad && ((uint64_t)lit_cursor + lpos + ll > nl || off > before + ll);
       const bool panic = valid && !dbad && !imp && ml != 0 && off == 0;
-      const uint64_t badm = __ballot(dbad || imp || panic);
+      // a match byte's state word is its distance to the byte it copies
+      // (< J_FINAL): only a frame past 2 GiB reaches further (the streaming
+      // K4 is no way out there: out of the GPU path's domain)
+      const bool far = valid && !dbad && !imp && !panic && ml != 0 && off + ml >= J_FINAL;
+      const uint64_t badm = __ballot(dbad || imp || panic || far);
       if (badm) {
         const int b = __ffsll((long long)badm) - 1;
+        const bool lim = __shfl((int)far, b, 64) != 0;
         const int code = __shfl(dbad ? bc : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b, 64);
-        if (lane == 0) key_min(fstate, JF.frame, make_key(PH_DECODE, D.j, DS_EXECUTE, s0 + (uint32_t)b, code));
+        if (lane == 0)
+          key_min(fstate, JF.frame, lim ? make_key(PH_LIMIT, D.j, LS_JROUNDS, s0 + (uint32_t)b, ZD_E_OUT_OF_DOMAIN)
+                                        : make_key(PH_DECODE, D.j, DS_EXECUTE, s0 + (uint32_t)b, code));
         return;
       }
       const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, k - 1);
@@ -4269,8 +4265,8 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
             if (rel < l) {
               w[b] = J_FINAL | (lsrc ? (uint32_t)lsrc[lp + rel] : lfill);
             } else {
-              const uint32_t jj = rel - l;
-              w[b] = pos + a + l - o + (jj < o ? jj : jj % o);
+              const uint32_t jj = rel - l;     // distance: o, or o times the periods passed
+              w[b] = o + (jj < o ? 0u : jj - jj % o);
             }
           }
         }
@@ -4297,83 +4293,129 @@ __device__ inline uint32_t j_frame_of(const JFrame* __restrict__ jframes, uint32
   return lo;
 }
 
-// One piece (16 state words) in a pointer-jumping round: S[p] = S[S[p]] for
-// each pending word, repeated up to `hops` times while some word of the
-// piece is still pending (every version of a word is true of its byte, so
-// more hops per round only shorten the chains faster).  A piece inside one
-// match whose source run is contiguous reads it with four 16-byte loads;
-// otherwise one gather per pending word.  A piece whose words are all final
-// is emitted -- its bytes to the frame's output -- and marked done, so later
-// rounds skip it without touching its words.  Returns true when the piece is
-// still pending.
-__device__ inline bool j_piece(uint8_t* outbase, const FrameDesc* __restrict__ frames, FrameState* fstate,
-                               const JFrame* __restrict__ jframes, uint32_t n_jframes, uint32_t* jst, uint8_t* done,
-                               uint64_t pc, uint32_t hops, uint32_t last) {
-  if (done[pc]) return false;
-  const JFrame JF = jframes[j_frame_of(jframes, n_jframes, pc)];
-  const FrameState* S = &fstate[JF.frame];
-  if (S->key != KEY_NONE) return false;
-  const uint64_t total = S->out_len;
-  const uint64_t p0 = 16 * (pc - JF.piece0);
-  if (p0 >= total) return false;
-  const uint32_t nb = (uint32_t)min<uint64_t>(16, total - p0);
-  uint32_t* st = jst + JF.base;
-  uint32_t w[16];
-  j_load_words(st + p0, w);
-  bool changed = false;
-  uint32_t pm = 0;
-#pragma unroll
-  for (uint32_t b = 0; b < 16; b++) pm |= (b < nb && !(w[b] & J_FINAL)) ? (1u << b) : 0u;
-  for (uint32_t h = 0; h < hops && pm; h++) {
-    uint32_t contig = 1;
-#pragma unroll
-    for (uint32_t b = 0; b < 16; b++) contig &= (uint32_t)(w[b] == w[0] + b);
-    if (pm == 0xFFFFu && contig && w[0] + 16 <= total) {
-      j_load_words(st + w[0], w);                  // one contiguous source run
-    } else {
-      uint32_t v[16];
-#pragma unroll
-      for (uint32_t b = 0; b < 16; b++) v[b] = ((pm >> b) & 1) ? st[w[b] < total ? w[b] : 0] : w[b];
-#pragma unroll
-      for (uint32_t b = 0; b < 16; b++) w[b] = v[b];
-    }
-    changed = true;
-    pm = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 16; b++) pm |= (b < nb && !(w[b] & J_FINAL)) ? (1u << b) : 0u;
-  }
-  if (changed) j_store_words(st + p0, w, nb);
-  if (pm) {
-    if (last) key_min(fstate, JF.frame, make_key(PH_LIMIT, 0, LS_JROUNDS, 0, ZD_E_OUT_OF_DOMAIN));
-    return true;
-  }
-  u32x4 v = (u32x4){0u, 0u, 0u, 0u};
-#pragma unroll
-  for (uint32_t b = 0; b < 16; b++) v[b >> 2] |= (w[b] & 255) << (8 * (b & 3));
-  j_store16(outbase + frames[JF.frame].out + p0, v, nb);
-  done[pc] = 1;
-  return false;
-}
-
-// Pointer-jumping round r over the K4J frames' pieces (16 state words each).
-// Each XCD sweeps one contiguous eighth of the pieces in ascending order
-// (workgroups b and b + 8 share an XCD, speed only): match sources lie at
-// most a window behind, so they were updated earlier in the same round more
-// often and sit in that XCD's L2.  pend[r] counts the waves that left a
-// piece pending; a round after one that left none exits at once, so the
-// rounds launched for the deepest possible chain cost a launch each.
+typedef __attribute__((address_space(1))) uint32_t g_u32a1 __attribute__((aligned(1)));
+#ifndef ZD_JW_K
+#define ZD_JW_K 2
+#endif
+constexpr int JW_K = ZD_JW_K;   // pieces per lane in flight (each hop issues JW_K independent loads)
+// Pointer-jumping round r, one state word per lane: sixteen lanes (a DPP row)
+// take a piece, and each lane JW_K pieces at once, so a wave holds 4 * JW_K
+// consecutive pieces.  A hop is one load per pending word, S[p] = S[S[p]]:
+// the words of one match point at one contiguous source run, so a wave's 64
+// loads fall on a few cache lines (one piece per lane made each word a
+// lane-private gather), and the JW_K loads of a lane are independent, so a
+// wave keeps JW_K dependent chains in flight (the rounds are bound by the
+// latency of those chains: a wave walks ~200 tiles one after another).  A
+// piece whose sixteen words are final is emitted -- four dword stores -- and
+// marked done.  The grid is what fits on the chip at once (8 workgroups of
+// 256 per CU), each XCD sweeping one contiguous eighth of the pieces in
+// ascending order (workgroups b and b + 8 share an XCD, speed only): match
+// sources lie at most a window behind, so they were updated earlier in the
+// same round more often and sit in that XCD's L2.  pend[r] counts the waves
+// that left a piece pending; a round after one that left none exits at once.
+// The rounds past the second run as one launch of `sweeps` sweeps: no round
+// needs another's words in any order (every version of a word is true of its
+// byte, and every chain ends at a literal the scatter wrote), so each wave
+// sweeps its own pieces until it leaves none pending, and the tail of empty
+// rounds costs one launch instead of one each.
 __global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const FrameDesc* __restrict__ frames,
                                                    FrameState* fstate, const JFrame* __restrict__ jframes,
                                                    uint32_t n_jframes, uint64_t n_pieces, uint32_t* jst,
                                                    uint32_t* pend, uint8_t* done, uint32_t hops, uint32_t r,
-                                                   uint32_t last) {
+                                                   uint32_t last, uint32_t sweeps) {
   if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
   const uint32_t x = blockIdx.x & 7, nk = gridDim.x >> 3;
+  const uint32_t sub = threadIdx.x & 15, row = threadIdx.x >> 4, wrow = row & 3;
   const uint64_t R = (n_pieces + 7) / 8;
   bool mine = false;
-  for (uint64_t i = (uint64_t)(blockIdx.x >> 3) * 256 + threadIdx.x; i < R; i += (uint64_t)nk * 256) {
-    const uint64_t pc = x * R + i;
-    if (pc < n_pieces) mine |= j_piece(outbase, frames, fstate, jframes, n_jframes, jst, done, pc, hops, last);
+  for (uint32_t sw = 0; sw < sweeps; sw++) {
+  const bool fin = last && sw + 1 == sweeps;
+  mine = false;
+  for (uint64_t i0 = (uint64_t)(blockIdx.x >> 3) * (16 * JW_K); i0 < R; i0 += (uint64_t)nk * (16 * JW_K)) {
+    uint64_t pc[JW_K], p0[JW_K], total[JW_K];
+    uint32_t* st[JW_K];
+    uint32_t w[JW_K], fr[JW_K];
+    bool act[JW_K], pw[JW_K], had[JW_K];
+#pragma unroll
+    for (int k = 0; k < JW_K; k++) {
+      const uint64_t i = i0 + 16 * k + row;           // a wave's rows: four consecutive pieces per k
+      pc[k] = x * R + i;
+      act[k] = i < R && pc[k] < n_pieces;
+    }
+    JFrame JF[JW_K];
+    uint8_t dn[JW_K];
+#pragma unroll
+    for (int k = 0; k < JW_K; k++) {
+      JF[k] = act[k] ? jframes[j_frame_of(jframes, n_jframes, pc[k])] : JFrame{};
+      dn[k] = act[k] ? done[pc[k]] : (uint8_t)1;
+    }
+    uint64_t key[JW_K];
+#pragma unroll
+    for (int k = 0; k < JW_K; k++) {
+      act[k] = act[k] && !dn[k];
+      fr[k] = JF[k].frame;
+      st[k] = jst + JF[k].base;
+      p0[k] = 16 * (pc[k] - JF[k].piece0);
+      const FrameState* S = &fstate[fr[k]];
+      key[k] = act[k] ? S->key : KEY_NONE;
+      total[k] = act[k] ? S->out_len : 0;
+      // the word itself, in parallel with the frame's state (bounded by the region)
+      w[k] = act[k] && p0[k] + sub < JF[k].cap ? st[k][p0[k] + sub] : J_FINAL;
+    }
+#pragma unroll
+    for (int k = 0; k < JW_K; k++) {
+      act[k] = act[k] && key[k] == KEY_NONE && p0[k] < total[k];
+      const bool inw = act[k] && p0[k] + sub < total[k];
+      if (!inw) w[k] = J_FINAL;
+      pw[k] = !(w[k] & J_FINAL);
+      had[k] = pw[k];
+    }
+    for (uint32_t h = 0; h < hops; h++) {
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < JW_K; k++) any |= pw[k];
+      if (!__ballot(any)) break;
+      uint32_t v[JW_K];
+#pragma unroll
+      for (int k = 0; k < JW_K; k++) {
+        const uint64_t p = p0[k] + sub;
+        v[k] = pw[k] ? st[k][w[k] <= p ? p - w[k] : 0u] : w[k];
+      }
+#pragma unroll
+      for (int k = 0; k < JW_K; k++) {
+        if (pw[k]) {
+          // a final source hands over its byte, a pending one adds its distance
+          const uint32_t d = w[k] + v[k];
+          w[k] = (v[k] & J_FINAL) ? v[k] : (d < J_FINAL ? d : w[k]);
+        }
+        pw[k] = !(w[k] & J_FINAL);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < JW_K; k++) {
+      if (had[k]) st[k][p0[k] + sub] = w[k];
+      const uint64_t pm = __ballot(pw[k]);
+      const bool piece_pending = ((pm >> (16 * wrow)) & 0xFFFFull) != 0;
+      if (act[k] && piece_pending) {
+        mine = true;
+        if (fin && sub == 0) key_min(fstate, fr[k], make_key(PH_LIMIT, 0, LS_JROUNDS, 0, ZD_E_OUT_OF_DOMAIN));
+      }
+      if (act[k] && !piece_pending) {
+        // bytes of four lanes into each lane of the quad (quad_perm broadcasts)
+        const uint32_t bt = w[k] & 255;
+        const uint32_t d = qdpp<0x00>(bt) | (qdpp<0x55>(bt) << 8) | (qdpp<0xAA>(bt) << 16) | (qdpp<0xFF>(bt) << 24);
+        uint8_t* o = outbase + frames[fr[k]].out + p0[k];
+        const uint64_t nb = total[k] - p0[k];
+        if (nb >= 16) {
+          if ((sub & 3) == 0) *(g_u32a1*)(o + sub) = d;
+        } else if (sub < nb) {
+          o[sub] = (uint8_t)bt;
+        }
+        if (sub == 0) done[pc[k]] = 1;
+      }
+    }
+  }
+  if (!__ballot(mine)) break;                      // the wave's pieces are all emitted
   }
   const uint64_t bm = __ballot(mine);
   if ((threadIdx.x & 63) == 0 && bm) atomicAdd(&pend[r], 1u);
@@ -4615,15 +4657,19 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_jscatter, dim3(a.n_jseg), dim3(64), 0, s, a.src, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, (const JSeg*)jseg, jsd, jst);
-    const uint64_t gw = (a.j_pieces + 255) / 256;
-    const dim3 gr((uint32_t)(gw < 8192 ? (gw + 7) & ~7ull : 8192));   // a multiple of 8 (one eighth per XCD)
+    const uint64_t gw = (a.j_pieces + 16 * JW_K - 1) / (16 * JW_K);   // pieces per workgroup sweep
+    const uint64_t gmax = 8ull * a.cus;                              // what fits at once: 8 workgroups per CU
+    const dim3 gr((uint32_t)(gw < gmax ? (gw + 7) & ~7ull : (gmax + 7) & ~7ull));   // a multiple of 8 (one eighth per XCD)
     // rounds past the second with a smaller grid (it strides over every
     // piece): they are the deepest chains' tail, usually empty, and an
     // empty round then costs little more than its launch
     const dim3 gt(std::min<uint32_t>(gr.x, 1024u));
-    for (uint32_t r = 1; r <= a.j_rounds; r++)
+    // rounds 1 and 2 one launch each, the rest as one launch of sweeps
+    const uint32_t nr = a.j_rounds < 3 ? a.j_rounds : 3u;
+    for (uint32_t r = 1; r <= nr; r++)
       hipLaunchKernelGGL(zd_k_jround, r <= 2 ? gr : gt, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
-                         a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == a.j_rounds));
+                         a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == nr),
+                         r == nr ? a.j_rounds - nr + 1 : 1u);
     if ((e = dom(DOM_K4J, 1)) != hipSuccess) return e;
   }
   if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;

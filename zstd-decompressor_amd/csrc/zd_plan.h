@@ -214,12 +214,14 @@ ZD_HD void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hb
   }
   fd.out = c.out;
   fd.out_cap = cap;
-  // K4J: frames of many compressed blocks (u32 positions)
+  // K4J: frames of many compressed blocks, and any frame past the streaming
+  // K4's int32 positions (distances, zd_common.h)
   const bool to_j = X.out_len0 == 0 && !frame_failed_host && fd.nblocks && hf.ncomp && hf.d.kind == ZD_FRAME_ZSTD &&
                     cap <= K4J_MAX_FRAME_OUT &&
-                    (X.k4j_mode >= 0 ? X.k4j_mode == 1 : (X.k4j_auto && hf.ncomp >= X.k4j_min));
-  // the streaming K4 keeps int32 frame positions: larger frames with
-  // sequences that K4J does not take are outside the GPU path's domain
+                    (X.k4j_mode >= 0 ? X.k4j_mode == 1
+                                     : ((X.k4j_auto && hf.ncomp >= X.k4j_min) || cap > K4_MAX_FRAME_OUT));
+  // larger frames with sequences that K4J does not take (forced off, or past
+  // its 32 GiB) are outside the GPU path's domain
   if (!to_j && cap > K4_MAX_FRAME_OUT && seqs_in_frame)
     fs.key = plan_min(fs.key, make_key(PH_LIMIT, 0, 0, 0, ZD_E_OUT_OF_DOMAIN));
   if (to_j) {

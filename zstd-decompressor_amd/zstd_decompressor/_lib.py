@@ -168,6 +168,12 @@ def buf(data):
         return C.cast(arr, C.c_void_p), n, arr
     raise TypeError("bytes-like object required")
 
+def take(arr, n: int) -> bytes:
+    """The first n bytes of a ctypes byte array, one memcpy (a buffer view:
+    C.string_at's size is a C int, and a ctypes slice goes element by element)."""
+    return bytes(memoryview(arr).cast("B")[:n])
+
+
 # status codes mirrored from include/zd.h
 NOT_ENOUGH_BYTES, NOT_ENOUGH_BITS, MAX_READABLE_BITS_EXCEEDED = -1, -2, -3
 EMPTY_INPUT_DATA, NULL_BYTE, EMPTY_SLICE = -4, -5, -6

@@ -30,7 +30,7 @@ def run_plan(plan, p, n):
     """(status, output): zd_plan_decompress into a buffer sized from the plan;
     again with the size it reports when the output came out larger (a frame
     that decodes past its declared size is re-planned inside the call).  The
-    output is read back with one memcpy (C.string_at), not an element-wise
+    output is read back with one memcpy (_lib.take), not an element-wise
     ctypes slice (seconds per 100 MB)."""
     L = _lib.lib()
     cap = max(plan.info.out_bytes, 1)
@@ -43,7 +43,7 @@ def run_plan(plan, p, n):
         if ol.value <= cap:
             break
         cap = ol.value
-    return st, C.string_at(out, min(ol.value, cap))
+    return st, _lib.take(out, min(ol.value, cap))
 
 
 def _decompress(data: bytes, flags: int):

@@ -22,7 +22,7 @@ class DecodingContext:
         L.zd_context_decoded(self._h, None, 0, C.byref(n))
         out = (C.c_uint8 * max(n.value, 1))()
         _lib.check(L.zd_context_decoded(self._h, out, n.value, C.byref(n)), "decoded")
-        return C.string_at(out, n.value)
+        return _lib.take(out, n.value)
 
     @property
     def offsets(self):
