@@ -1840,9 +1840,6 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
-#ifndef ZD_K3_DPPASM
-#define ZD_K3_DPPASM 1
-#endif
 template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
@@ -1909,20 +1906,8 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     use = winn_load<N>(bs, m, pos);
     // the state bits sit OF | ML | LL upwards from y: offsets 0, nbO, nbO +
     // nbM (the shadow takes the LL lane's), by quad_perm [0,0,1,1] twice
-#if ZD_K3_DPPASM
-    // the same two quad_perm [0,0,1,1] steps as one v_and_b32_dpp and one
-    // v_add_u32_dpp (DPP on src0; s_nop 1: a DPP read of a VGPR written by
-    // the previous VALU op needs two wait states): two VALU ops on the chain
-    // instead of four
-    uint32_t t, o;
-    asm volatile("s_nop 1\n\tv_and_b32_dpp %0, %2, %3 quad_perm:[0,0,1,1] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 1\n\tv_add_u32_dpp %1, %0, %0 quad_perm:[0,0,1,1] row_mask:0xf bank_mask:0xf"
-                 : "=&v"(t), "=v"(o) : "v"(nb), "v"(m0));
-    const uint32_t v = __builtin_amdgcn_ubfe(r, o, nb);
-#else
     const uint32_t t = qdpp<0x50>(nb) & m0;
     const uint32_t v = __builtin_amdgcn_ubfe(r, t + qdpp<0x50>(t), nb);
-#endif
     s = (ns << nb) + v - Tr;   // (the next address formed from v in one op: 2.07 -> 2.11 ms on C3)
   };
   uint32_t i = 0;
