@@ -117,6 +117,43 @@ def test_fuzz_forked_plans():
     assert seen["ood"] == 0, seen
 
 
+def _seeds_multi_block():
+    """Frames of several blocks (the block-parallel executor K4J's inputs)."""
+    src = gen.text(700_000, seed=12)
+    return [libzstd.compress(src[:450_000], 3), libzstd.compress(gen.xml(300_000, seed=13), 19),
+            libzstd.compress(gen.binary(260_000, seed=14), 1), gen.frames(src, 300_000, 9)]
+
+
+def test_fuzz_block_parallel():
+    """The mutations on frames of several blocks, half of them forced onto
+    K4J (ZD_F_BLOCK_PARALLEL: scatter checks, pointer-jumping rounds, the
+    per-block prefix of repeat offsets), the rest on the automatic routing
+    (K4J for frames of >= 2 compressed blocks in plans of <= 64 frames).
+    ZD_FUZZ_ITERS / 4 inputs (default 150)."""
+    from zstd_decompressor import _lib
+    from zstd_decompressor.batch import decompress_status
+    iters = int(os.environ.get("ZD_FUZZ_ITERS", "600")) // 4
+    r = random.Random(int(os.environ.get("ZD_FUZZ_SEED", str(0xF022)), 0) + 2)
+    seeds = _seeds_multi_block()
+    seen = {"ok": 0, "err": 0, "ood": 0}
+    for it in range(iters):
+        data = _mutate(r, seeds)
+        p = r.random() < 0.3
+        flags = _lib.F_BLOCK_PARALLEL if r.random() < 0.5 else 0
+        ost, oout = oracle.decompress_status(data, p)
+        gst, gout = decompress_status(data, p, flags)
+        if gst == OUT_OF_DOMAIN:
+            seen["ood"] += 1
+            _dump_ood(data, p, f"bp{it}")
+            continue
+        assert gst == ost, f"#{it}: oracle {ost}, gpu {gst}"
+        same = gout == oout                           # (no pytest diff of large bytes)
+        assert same, f"#{it}: output differs ({len(gout)} vs {len(oout)} bytes)"
+        seen["ok" if ost == 0 else "err"] += 1
+    print("fuzz outcome counts (block-parallel):", seen)
+    assert seen["ood"] == 0, seen
+
+
 # (seed, input index) of campaign inputs that once disagreed with the oracle
 REGRESSIONS = [
     (6, 4281),     # runaway Huffman-weight stream before a reserved sequence-mode bit: oracle REF_PANIC
