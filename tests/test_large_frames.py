@@ -147,3 +147,43 @@ def test_single_frame_over_2GiB():
     assert gout == src
     del gout
     assert _gpu(data, fs)[0] == OUT_OF_DOMAIN
+
+
+_UNCONVERGED = r"""
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/zstd-decompressor_amd"]
+from corpus import gen, libzstd
+from zstd_decompressor import _lib
+from zstd_decompressor.batch import Plan, run_plan
+tile = gen.text(4096, seed=15)
+src = b"".join(bytes([i & 255]) + tile for i in range(1200))      # every tile copies the one before
+for s in (src, gen.text(3_000_000, seed=16)):
+    data = libzstd.compress(s, 3)
+    p = Plan(data, False, _lib.F_BLOCK_PARALLEL)
+    pp, n, keep = _lib.buf(data)
+    st, out = run_plan(p, pp, n)
+    print(st, int(out == s), p.refresh_info().replans, flush=True)
+    p.close()
+"""
+
+
+def test_block_parallel_unconverged_replans(tmp_path):
+    """K4J with its pointer jumping cut to one round of one hop (ZD_J_ROUNDS,
+    ZD_J_HOPS: the rounds' last sweep finds pending pieces): the frame keys
+    LS_JROUNDS and zd_plan_decompress plans it again on the streaming
+    executor -- same bytes, one re-plan.  In a child process (the knobs are
+    read once per process)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "unconverged.py"
+    script.write_text(_UNCONVERGED)
+    env = dict(os.environ, ZD_J_ROUNDS="1", ZD_J_HOPS="1")
+    r = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l.split() for l in r.stdout.strip().splitlines()]
+    assert len(lines) == 2, r.stdout
+    for st, same, replans in lines:
+        assert st == "0" and same == "1", r.stdout
+    assert any(int(x[2]) >= 1 for x in lines), r.stdout   # the deep chains did not converge in one hop

@@ -133,10 +133,10 @@ ZD_HD inline void rec_pack(uint32_t posA, uint32_t stA, uint32_t posB, uint32_t 
 // the chains write past the last)
 ZD_HD inline uint64_t rec_slots(uint32_t n) { return n ? ((uint64_t)(n + 1) & ~1ull) + 2 : 0; }
 constexpr uint32_t DIRECT_GIANT = (1u << 29) - 1;
-// Output bounds per executor: the streaming K4 keeps int32 frame positions,
-// K4J 31-bit ones in its state words; a frame with sequences above both is
-// outside the GPU path's domain (ZD_E_OUT_OF_DOMAIN; the reference's own
-// limit is the 8 MiB window).
+// Output bounds per executor: the streaming K4 keeps int32 frame positions;
+// K4J u64 positions and 31-bit distances in its state words, up to 32 GiB a
+// frame.  A frame with sequences above both is outside the GPU path's domain
+// (ZD_E_OUT_OF_DOMAIN; the reference's own limit is the 8 MiB window).
 constexpr uint64_t K4_MAX_FRAME_OUT = 0x7FFF0000ull;
 constexpr uint64_t K4J_MAX_FRAME_OUT = 1ull << 35;   // 32 GiB: 128 GiB of K4J state words
 constexpr uint64_t OFF_HUGE = ~0ull >> 1;        // a giant offset (never <= a decoded length)

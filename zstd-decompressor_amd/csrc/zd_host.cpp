@@ -1603,7 +1603,11 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_jframes = (uint32_t)P->n_jframes;
   a.n_jblk = (uint32_t)P->n_jblk;
   a.n_jseg = (uint32_t)P->n_jseg;
-  a.j_rounds = P->j_rounds;
+  // ZD_J_ROUNDS caps the rounds (a test of the path that re-plans a frame
+  // whose pointer jumping did not converge on the streaming executor)
+  static const char* rounds_env = getenv("ZD_J_ROUNDS");
+  a.j_rounds = rounds_env && P->j_rounds ? std::min<uint32_t>(P->j_rounds, (uint32_t)std::max(1, atoi(rounds_env)))
+                                         : P->j_rounds;
   a.j_pieces = P->j_pieces;
   // hops per pending word and K4J round (c3s, scripts/exp_jhops.sh: 1 hop
   // 10.2 ms, 2 5.2, 4 3.0, 8 2.44, 16 2.67, 32 2.95); ZD_J_HOPS overrides
