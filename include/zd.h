@@ -399,7 +399,9 @@ int zd_block_decode(zd_context* ctx, const uint8_t* src, size_t n,
                     size_t* consumed, int* last);
 
 /* DecodingContext::execute_sequences (decoding_context.rs:78-106) on the
- * GPU: sequences are (literals_length, offset_value, match_length). */
+ * GPU: sequences are (literals_length, offset_value, match_length), any u32
+ * values.  ZD_E_OUT_OF_DOMAIN when the context's output would pass
+ * 2^31 - 64 KiB (the streaming executor's positions). */
 int zd_execute_sequences(zd_context* ctx, const uint32_t* ll,
                          const uint32_t* offset_value, const uint32_t* ml,
                          size_t nseq, const uint8_t* literals, size_t nlits);

@@ -61,6 +61,44 @@ def test_execute_sequences_kat(kat):
         assert ctx.decoded == bytes(c["out"]), c["src"]
 
 
+def test_execute_sequences_large_values():
+    """DecodingContext.execute_sequences with values past the direct records'
+    packed fields (literals_length >= 2^17 - 1, match_length >= 2^18 - 1,
+    offset_value >= 2^29 - 1): escape records whose exact triple the executor
+    reads from a side array.  Long literal runs, long overlapping and
+    non-overlapping matches, repeat codes after them, and offsets past the
+    output (ImpossibleValue), against the oracle's DecodingContext."""
+    import random
+    from zstd_decompressor import DecodingContext, ZdError
+    r = random.Random(77)
+    lits = bytes(r.randrange(256) for _ in range(700_000))
+    cases = [
+        [(200_000, 4, 300_000)],                                   # a long literal run, then an RLE-like match
+        [(131_071, 5000 + 3, 262_143), (0, 1, 7), (9, 2, 300_000), (3, 3, 12)],   # exactly at the field maxima
+        [(150_000, 140_000 + 3, 140_000), (1, 1, 270_000), (70_000, 3, 5)],       # long copies, repeat codes
+        [(10, (1 << 29) + 10, 4)],                                 # an offset past the output: ImpossibleValue
+        [(262_144, 200_000 + 3, 1 << 18), (0, (1 << 31) + 7, 3)],  # a giant offset after a long run
+    ]
+    for i, seqs in enumerate(cases):
+        try:
+            want, werr = oracle.execute_sequences(seqs, lits, cap=4 << 20), None
+        except Exception as e:                                     # the oracle's error variant
+            want, werr = None, getattr(e, "code", e)
+        ctx = DecodingContext(8 << 20)
+        try:
+            ctx.execute_sequences(seqs, lits)
+            got, gerr = ctx.decoded, None
+        except ZdError as e:
+            got, gerr = None, e.code
+        ctx.close()
+        assert (werr is None) == (gerr is None), f"case {i}: oracle {werr}, gpu {gerr}"
+        if werr is None:
+            same = got == want
+            assert same, f"case {i}: {len(got)} vs {len(want)} bytes"
+        else:
+            assert gerr == werr, f"case {i}: oracle {werr}, gpu {gerr}"
+
+
 def test_context_block_by_block(resources):
     """Block.parse + Block.decode(ctx) over moby-dick's blocks == Frame.decode
     (tests/block.rs usage pattern with DecodingContext::new(MAX_WIN_SIZE))."""

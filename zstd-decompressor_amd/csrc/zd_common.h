@@ -147,6 +147,24 @@ ZD_HD inline uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t ofv) {
 ZD_HD inline uint32_t seq_ll(uint64_t s) { return (uint32_t)(s & 0x1FFFF); }
 ZD_HD inline uint32_t seq_ml(uint64_t s) { return (uint32_t)((s >> 17) & 0x3FFFF); }
 ZD_HD inline uint32_t seq_off(uint64_t s) { return (uint32_t)(s >> 35); }
+// A direct record with a field at its maximum (literals_length >= 2^17 - 1,
+// match_length >= 2^18 - 1 or offset_value >= DIRECT_GIANT) is an escape:
+// its exact values are the record's DirectSide entry (CompBlock::seq_side,
+// same index), so the context API takes any u32 triple.
+struct DirectSide { uint32_t ll, ml, ofv, pad; };
+constexpr uint64_t DIRECT_ESCAPE = (uint64_t)0x1FFFF | ((uint64_t)0x3FFFF << 17) | ((uint64_t)DIRECT_GIANT << 35);
+ZD_HD inline bool seq_escaped(uint64_t s) {
+  return seq_ll(s) == 0x1FFFF || seq_ml(s) == 0x3FFFF || seq_off(s) == DIRECT_GIANT;
+}
+// record i's values (side: the block's DirectSide entries)
+ZD_HD inline void seq_values(uint64_t s, uint64_t side, uint32_t i, uint32_t* ll, uint32_t* ml, uint32_t* ofv) {
+  if (side && seq_escaped(s)) {
+    const DirectSide d = ((const DirectSide*)side)[i];
+    *ll = d.ll; *ml = d.ml; *ofv = d.ofv;
+  } else {
+    *ll = seq_ll(s); *ml = seq_ml(s); *ofv = seq_off(s);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Repeat-offset codes (u32) for resolving decode_offset (decoding_context.rs:
@@ -319,6 +337,8 @@ struct CompBlock {
   uint64_t src;            // absolute offset of the block content in d_src
   uint64_t lit_out;        // byte offset of this block's literals in the literal workspace
   uint64_t seq_out;        // sequence index of this block's first sequence in the sequence workspace
+  uint64_t seq_side;       // direct records (zd_execute_sequences): device address of their DirectSide
+                           // entries (values past the packed fields), 0 when none
   uint32_t size;           // Block_Size
   uint32_t frame;          // plan frame index
   uint32_t block_in_frame;

@@ -2251,6 +2251,8 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   // and whose sequences are pre-decoded: only the execute kernel runs.
   uint64_t need = c->len + nlits;
   for (size_t i = 0; i < nseq; i++) need += ml[i];
+  // the streaming K4's int32 positions bound the context's output
+  if (need >= K4_MAX_FRAME_OUT) return ZD_E_OUT_OF_DOMAIN;
   if (int r = ctx_reserve(c, need + 16)) return r;
   zd_plan P;
   HostFrame hf;
@@ -2275,35 +2277,46 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   }
   int32_t none[3] = {-1, -1, -1};
   uint64_t rep0[3] = {c->rep[0], c->rep[1], c->rep[2]};
+  P.flags |= ZD_F_FRAME_SERIAL;         // the streaming K4 (K4J reads no direct records)
   build_plan(&P, -1, none, c->len, rep0, c->d_cap);
   P.list_tables.clear();
   P.list_huf.clear();
   P.list_seq.clear();   // sequences come from the caller
   P.info.src_bytes = nlits;
-  int r = upload_plan(&P);
+  // the caller's triples as direct records (zd_common.h): a value past its
+  // packed field is an escape with its exact triple in a DirectSide entry
+  uint8_t* d_side = nullptr;
   auto fin = [&](int rr) {
     ws_release(P.d_ws, P.ws_bytes, P.dev);
     if (P.d_staging) (void)hipFree(P.d_staging);
-    P.d_ws = nullptr; P.d_staging = nullptr;
+    if (d_side) (void)hipFree(d_side);
+    P.d_ws = nullptr; P.d_staging = nullptr; d_side = nullptr;
     return rr;
   };
+  std::vector<uint64_t> rec(nseq);
+  std::vector<DirectSide> side;
+  if (nseq) {
+    for (size_t i = 0; i < nseq; i++) {
+      const bool esc = ll[i] >= 0x1FFFF || ml[i] >= 0x3FFFF || ofv[i] >= DIRECT_GIANT;
+      if (esc && side.empty()) side.assign(nseq, DirectSide{});
+      if (esc) side[i] = DirectSide{ll[i], ml[i], ofv[i], 0};
+      rec[i] = esc ? DIRECT_ESCAPE : seq_pack(ll[i], ml[i], ofv[i]);
+    }
+    if (!side.empty()) {
+      if (hipMalloc(&d_side, side.size() * sizeof(DirectSide)) != hipSuccess) { d_side = nullptr; return fin(ZD_E_NO_MEMORY); }
+      if (hipMemcpy(d_side, side.data(), side.size() * sizeof(DirectSide), hipMemcpyHostToDevice) != hipSuccess)
+        return fin(ZD_E_HIP);
+      P.comps[0].seq_side = (uint64_t)(uintptr_t)d_side;
+    }
+  }
+  int r = upload_plan(&P);
   if (r) return fin(r);
   const hipStream_t s = c->s;
   if (int rr = ctx_input(c, lits, nlits)) return fin(rr);
-  // the caller's triples as direct records (zd_common.h); offsets are
-  // exact below DIRECT_GIANT, which stays past every decoded length here
   CompState cs{};
   cs.lit_count = (uint32_t)nlits;
-  std::vector<uint64_t> rec(nseq);
-  if (nseq) {
-    if (need >= DIRECT_GIANT - 3) return fin(ZD_E_OUT_OF_DOMAIN);
-    for (size_t i = 0; i < nseq; i++) {
-      if (ll[i] > 0x1FFFF || ml[i] > 0x3FFFF) return fin(ZD_E_OUT_OF_DOMAIN);
-      rec[i] = seq_pack(ll[i], ml[i], ofv[i]);
-    }
-    if (hipMemcpyAsync(P.d_ws + P.W.seqs, rec.data(), nseq * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-      return fin(ZD_E_HIP);
-  }
+  if (nseq && hipMemcpyAsync(P.d_ws + P.W.seqs, rec.data(), nseq * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+    return fin(ZD_E_HIP);
   P.fdesc[0].out = 0;
   if (hipMemcpyAsync(P.d_ws + P.W.comp_state, &cs, sizeof cs, hipMemcpyHostToDevice, s) != hipSuccess ||
       hipMemcpyAsync(P.d_ws + P.W.frames, P.fdesc.data(), sizeof(FrameDesc), hipMemcpyHostToDevice, s) != hipSuccess ||

@@ -2575,8 +2575,8 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         bool giant = false;
         if (valid) {
           if (direct) {
-            ll = seq_ll(recA); ml = seq_ml(recA); ofv = seq_off(recA);
-            giant = ofv == DIRECT_GIANT;
+            seq_values(recA, C.seq_side, i, &ll, &ml, &ofv);
+            giant = ofv == DIRECT_GIANT && !C.seq_side;
           } else {
             const uint32_t stt = (uint32_t)(recA >> 32);
             const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
@@ -3516,7 +3516,7 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
         if (b0 + k < cn) {
           const uint64_t sq = rec_get(SQ, c0 + b0 + k, direct);
           if (direct) {
-            ll[k] = seq_ll(sq); ml[k] = seq_ml(sq); oc[k] = seq_off(sq);
+            seq_values(sq, C.seq_side, c0 + b0 + k, &ll[k], &ml[k], &oc[k]);
           } else {
             const int32_t bp = (int32_t)(uint32_t)sq;
             const uint32_t stt = (uint32_t)(sq >> 32);
