@@ -34,6 +34,8 @@ for s in "$@"; do
     pmcj) run pmc_j1 300 rocprofv3 --kernel-trace --kernel-include-regex "zd_k_jround|zd_k_jscatter" --pmc SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU -d gpurun_out/pmc_j1 -o run --output-format csv -- python bench.py --workload c3s --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io && run pmc_j2 300 rocprofv3 --kernel-trace --kernel-include-regex "zd_k_jround|zd_k_jscatter" --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum -d gpurun_out/pmc_j2 -o run --output-format csv -- python bench.py --workload c3s --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io ;;
     c3senv:*) e=${s#c3senv:}; run bench_c3s_env_${e//[=,]/_} 600 env ${e//,/ } python bench.py --workload c3s --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     c3var:*) v=${s#c3var:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run bench_c3_$v 600 python bench.py --workload c3 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
+    c2bigvar:*) v=${s#c2bigvar:}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c2big_$v 600 python bench.py --workload c2 --c2-mib 1024 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
+    c2var:*) v=${s#c2var:}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c2_$v 600 python bench.py --workload c2 --steps 20 --warmup 5 --no-cpu-baseline --no-host-io ;;
     benchc3) run bench_c3 600 python bench.py --workload c3 --steps 5 --warmup 2 --no-cpu-baseline ;;
     nofarq) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_nofar.so run bench_nofar 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify --experiment --no-host-io ;;
     k3q8q) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-host-io ;;
