@@ -4294,7 +4294,7 @@ typedef __attribute__((address_space(1))) uint32_t g_u32a1 __attribute__((aligne
 constexpr int JW_K = ZD_JW_K;   // pieces per lane in flight (each hop issues JW_K independent loads)
 // Pointer-jumping round r, one state word per lane: sixteen lanes (a DPP row)
 // take a piece, and each lane JW_K pieces at once, so a wave holds 4 * JW_K
-// consecutive pieces.  A hop is one load per pending word, S[p] = S[S[p]]:
+// consecutive pieces.  A hop is one load per pending word, S[p] = S[p - S[p]]:
 // the words of one match point at one contiguous source run, so a wave's 64
 // loads fall on a few cache lines (one piece per lane made each word a
 // lane-private gather), and the JW_K loads of a lane are independent, so a
