@@ -186,7 +186,7 @@ def huffman_parse_decode(desc: bytes, stream: bytes, cap=1 << 20):
 
 def huffman_widths(desc: bytes):
     L = lib(); d, dn = _buf(desc)
-    w = (C.c_uint8 * 4096)(); nw = C.c_size_t(); cons = C.c_size_t(); e = _Err()
+    w = (C.c_uint8 * (1 << 18))(); nw = C.c_size_t(); cons = C.c_size_t(); e = _Err()   # (>= the weights a 127-byte stream can give)
     r = L.zdo_huffman_widths(d, dn, w, C.byref(nw), C.byref(cons), C.byref(e))
     _check(r, e)
     return cons.value, list(w)[: nw.value]

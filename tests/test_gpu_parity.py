@@ -627,6 +627,67 @@ def test_k2_trees_deeper_than_the_lut():
     assert ost == 0
 
 
+# FSE-compressed Huffman weights decoding to 7,709 nonzero weights (maxBits 13):
+# more leaves than a LUT slot's 7,680 symbol bytes (tests/golden/make_deep_tree_desc.py)
+DEEP_DESC_7709 = bytes.fromhex(
+    "7621fc01f0bfd64950ebd9ef23d79f8cf8023d4fd669ffba7efbdffbae8bcaa6ae366df908c7266acb382b4d79de8c"
+    "fac3345fe9099c6a0b85c60ef9beef7bb5c5eba739082a8c150f08ff8feb5c1d9bc050f0fda7c7fbc351db16d35479"
+    "bbbe61212d2594467f7676fe5b7f2288477b40d32af17affe0")
+
+
+def _big_tree_frame(r, codes, n):
+    """One frame, one compressed block: DEEP_DESC_7709's tree over n literals
+    encoded with its codes (insertion order of huffman.rs:132-175; the first
+    literal's code right under the marker bit), then one sequence from random
+    bits with the predefined tables."""
+    keys = list(codes)
+    v = 1
+    for _ in range(n):
+        c, w = codes[r.choice(keys)]
+        v = (v << w) | c
+    stream = v.to_bytes((v.bit_length() + 7) // 8, "little")
+    comp = len(DEEP_DESC_7709) + len(stream)
+    lh = (2 | (0 << 2) | (n << 4) | (comp << 14)).to_bytes(3, "little")   # compressed, 1 stream
+    seqs = bytes([1, 0x00]) + bytes(r.randrange(256) for _ in range(4)) + bytes([r.randrange(1, 256)])
+    content = lh + DEEP_DESC_7709 + stream + seqs
+    hdr = ((len(content) << 3) | (2 << 1) | 1).to_bytes(3, "little")
+    return b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x50]) + hdr + content
+
+
+def test_k2_tree_past_the_lut_slot():
+    """A deep tree with more leaves (7,709) than a LUT slot's symbol bytes:
+    K1's huge pass keeps its symbols in the plan's deep pool (zd_kernels.hip
+    deep_build, DEEP_IN_POOL) and K2 decodes from there.  Frames that decode
+    and frames the reference rejects (its sequence is random), alone and many
+    of them in one plan beside libzstd frames (several trees in the pool)."""
+    _, widths = oracle.huffman_widths(DEEP_DESC_7709)
+    p = max(widths)
+    assert p == 13 and sum(1 for w in widths if w) > 7680
+    codes, pos = {}, 0
+    for w in range(p, 0, -1):                      # longest first, ascending symbols, aligned slots
+        S = 1 << (p - w)
+        al = (pos + S - 1) & ~(S - 1)
+        for i in (i for i, x in enumerate(widths) if x == w):
+            if al + S > 1 << p:
+                break
+            codes[i] = (al >> (p - w), w)
+            al += S
+        pos = al
+    r = random.Random(31)
+    ok = []
+    for i in range(120):
+        f = _big_tree_frame(r, codes, r.randrange(100, 500))
+        ost, _ = assert_parity(f, False, f"tree of 7,709 leaves #{i}")
+        if ost == 0:
+            ok.append(f)
+    assert len(ok) >= 3
+    src = gen.text(200_000, seed=6)
+    parts = []
+    for i in range(12):
+        parts.append(ok[i % len(ok)] if i % 2 else gen.frames(src[i * 12_000:(i + 1) * 12_000], 12_000, 3))
+    ost, _ = assert_parity(b"".join(parts), False, "trees of 7,709 leaves inside libzstd frames")
+    assert ost == 0
+
 def _pair_table_kind(weights):
     """Which pair-table entries a tree of direct weights gives K2
     (zd_kernels.hip PR_*): None when the reference panics building it, else

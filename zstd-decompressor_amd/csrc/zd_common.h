@@ -30,6 +30,9 @@ constexpr uint16_t LUT_ABSENT = 0x8000;
 // Every sequence code above 63 is already past LL/ML/OF maxima (35/52/31) and
 // every Huffman weight above 32 already panics, so the clamp keeps behaviour.
 constexpr int FSE_TAB = 1 << FSE_MAX_AL;           // u16 entries per table in a slot
+// K1's pool for the symbols of deep Huffman trees with more leaves than a
+// LUT slot holds (only a weight stream of > 7,680 nonzero weights makes one)
+constexpr uint64_t DEEP_POOL_BYTES = 4ull << 20;
 constexpr int FSE_SLOT = 3 * FSE_TAB;              // LL | OF | ML
 ZD_HD inline uint16_t fse_entry(uint32_t sym, uint32_t ns) { return (uint16_t)((sym > 63 ? 63 : sym) | (ns << 6)); }
 ZD_HD inline int hb32(uint32_t v) {
@@ -470,6 +473,7 @@ struct Workspace {
   uint64_t jframes, jblkd, jblk, jseg, jsegd, jpend;    // K4J descriptors / state / round counters
   uint64_t jdone;                                       // K4J: one byte per piece, 1 once emitted
   uint64_t huge;                                        // K1: u32 count + the blocks whose trees have > 256 symbols
+  uint64_t deep;                                        // K1's pool for deep trees of > 7,680 leaves: u32 used, then bytes
   uint64_t jst;                                         // K4J per-byte state words
   uint64_t redo, k2done;                                // zd_k_fused: frames for the redo pass, K2's finished workgroups
   uint64_t hframes;                                     // device-built plans: the walk's frame index (zd_walk.h HostFrame)

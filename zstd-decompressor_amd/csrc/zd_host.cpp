@@ -409,6 +409,7 @@ void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint
   auto carve = [&](uint64_t bytes) { uint64_t r = o; o = align_up(o + bytes, 256); return r; };
   W.comp_state = carve(sizeof(CompState) * std::max<uint64_t>(T.comps, 1));
   W.huge = carve(4 * (std::max<uint64_t>(T.tables, 1) + 1));
+  W.deep = carve(16 + (T.luts ? DEEP_POOL_BYTES : 0));
   W.frame_state = carve(sizeof(FrameState) * std::max<uint64_t>(T.frames, 1));
   W.lits = carve(T.lits + 64);
   W.seqs = carve(8 * T.nrec + 64);
@@ -1584,6 +1585,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
                         P->n_frames * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<uint64_t>(P->n_comps, 1) * sizeof(CompState), s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.huge, 0, 4, s));   // K1's list of trees of more than 256 symbols
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.deep, 0, 4, s));   // and its deep-tree symbol pool
   if (P->n_jframes) {
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jdone, 0, std::max<uint64_t>(P->j_pieces, 1), s));
@@ -2064,6 +2066,7 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   const hipStream_t s = c->s;
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<size_t>(P->comps.size(), 1) * sizeof(CompState), s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.huge, 0, 4, s));
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.deep, 0, 4, s));
   // prebuilt comp 0 carries the context's tables
   CompState pcs{};
   if (P->has_prebuilt) {

@@ -399,12 +399,38 @@ __device__ void lut_holes(uint16_t* __restrict__ lut, int p, uint32_t a, uint32_
 // writes the first k of them.  K2 decodes these blocks with huf_stream_deep.
 constexpr uint32_t DEEP_SYMS_AT = 512;
 constexpr uint32_t DEEP_SYM_CAP = LUT_ENTRIES * 2 - DEEP_SYMS_AT;
+constexpr uint32_t DEEP_IN_POOL = 1u << 31;      // tab[0]: the symbols are in the pool, at tab[DEEP_POOL_AT]
+constexpr uint32_t DEEP_POOL_AT = DEEP_SYMS_AT / 4 - 1;   // (past 31 groups of 4 words)
+// A tree with more placed leaves than the slot's DEEP_SYM_CAP bytes keeps its
+// symbols in the plan's deep pool (pool_used: the pool's u32 fill counter,
+// the bytes follow it 16 bytes on); past the pool it is out of the domain.
 template <typename COUNT, typename EMIT>
-__device__ int deep_build(uint32_t* tab, int p, COUNT count, EMIT emit) {
+__device__ int deep_build(uint32_t* tab, int p, COUNT count, EMIT emit, uint32_t* pool_used = nullptr) {
   const uint64_t T = 1ull << p;
   uint64_t pos = 0;
-  uint32_t G = 0, off = 0;
+  uint32_t G = 0, off = 0, flag = 0;
   uint8_t* syms = (uint8_t*)tab + DEEP_SYMS_AT;
+  {
+    uint64_t q = 0, total = 0;                    // the leaves the insertion places
+    for (int w = p; w >= 1; w--) {
+      const uint32_t c = count(w);
+      if (!c) continue;
+      const uint64_t S = 1ull << (p - w);
+      const uint64_t al = (q + S - 1) & ~(S - 1);
+      const uint64_t fit = (T - al) / S;
+      const uint64_t k = c < fit ? c : fit;
+      q = al + k * S;
+      total += k;
+    }
+    if (total > DEEP_SYM_CAP) {
+      if (!pool_used) return ZD_E_OUT_OF_DOMAIN;
+      const uint32_t at = atomicAdd(pool_used, (uint32_t)total);
+      if ((uint64_t)at + total > DEEP_POOL_BYTES) return ZD_E_OUT_OF_DOMAIN;
+      syms = (uint8_t*)pool_used + 16 + at;
+      tab[DEEP_POOL_AT] = at;
+      flag = DEEP_IN_POOL;
+    }
+  }
   for (int w = p; w >= 1; w--) {
     const uint32_t c = count(w);
     if (!c) continue;
@@ -414,7 +440,6 @@ __device__ int deep_build(uint32_t* tab, int p, COUNT count, EMIT emit) {
     const uint32_t k = (uint32_t)(c < fit ? c : fit);
     pos = al + k * S;
     if (!k) continue;
-    if (off + k > DEEP_SYM_CAP) return ZD_E_OUT_OF_DOMAIN;   // (trees of > 7,680 leaves)
     tab[1 + 4 * G] = (uint32_t)al;
     tab[2 + 4 * G] = (uint32_t)pos;
     tab[3 + 4 * G] = (uint32_t)w;
@@ -423,7 +448,7 @@ __device__ int deep_build(uint32_t* tab, int p, COUNT count, EMIT emit) {
     off += k;
     G++;
   }
-  tab[0] = G;
+  tab[0] = G | flag;
   return 0;
 }
 
@@ -731,7 +756,7 @@ struct K1LaneH {
 };
 
 __device__ int k1_huffman_huge(const uint8_t* desc, const uint8_t* src, const uint8_t* src_end, K1LaneH& L,
-                               uint16_t* lut, int* p_out) {
+                               uint16_t* lut, int* p_out, uint32_t* deep) {
   uint32_t sum = 0, maxw = 0, nw = 0;
   bool panic = false;
   int st = k1_weight_stream(desc, src, src_end, L, [&](uint32_t, uint32_t w) {
@@ -772,7 +797,8 @@ __device__ int k1_huffman_huge(const uint8_t* desc, const uint8_t* src, const ui
                         uint32_t r = 0;
                         for (int b = 0; b < 256 && r < k; b++)
                           for (uint32_t c = L.cnt[w][b]; c > 0 && r < k; c--) dst[r++] = (uint8_t)b;
-                      });
+                      },
+                      deep);
   }
   const uint32_t T = 1u << p;
   uint32_t pos = 0;
@@ -808,7 +834,7 @@ __device__ int k1_huffman_huge(const uint8_t* desc, const uint8_t* src, const ui
 __global__ __launch_bounds__(K1H_LANES) void zd_k_tables_huge(const uint8_t* __restrict__ src, uint64_t src_size,
                                                               const CompBlock* __restrict__ comp, CompState* cstate,
                                                               FrameState* fstate, const uint32_t* __restrict__ huge,
-                                                              uint16_t* luts) {
+                                                              uint16_t* luts, uint32_t* deep) {
   __shared__ K1LaneH lanes[K1H_LANES];
   K1LaneH& L = lanes[threadIdx.x];
   const uint32_t n = huge[0];
@@ -817,7 +843,7 @@ __global__ __launch_bounds__(K1H_LANES) void zd_k_tables_huge(const uint8_t* __r
     const CompBlock C = comp[ci];
     int p = 0;
     const int st = k1_huffman_huge(src + C.src + C.lit_data, src, src + src_size, L,
-                                   luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p);
+                                   luts + (uint64_t)C.lut_slot * LUT_ENTRIES, &p, deep);
     if (st == ZD_E_OUT_OF_DOMAIN)
       key_min(fstate, C.frame, make_key(PH_DECODE, C.block_in_frame, DS_LITERALS, 0, ZD_E_OUT_OF_DOMAIN));
     else if (st)
@@ -1275,15 +1301,15 @@ __device__ int huf_stream(const uint8_t* bs, uint32_t size, uintptr_t base, g_u1
 // of the gap around it (as lut_holes).  The reference's checks as in
 // huf_stream's tail.
 __device__ int huf_stream_deep(const uint8_t* bs, uint32_t size, uintptr_t base, const uint32_t* tab, int p,
-                               uint8_t* out, uint32_t cap, uint32_t* count_out) {
+                               uint8_t* out, uint32_t cap, uint32_t* count_out, const uint8_t* pool) {
   uint32_t count = 0;
   *count_out = 0;
   if (size == 0) return ZD_E_EMPTY_INPUT_DATA;
   const uint8_t lastb = bs[size - 1];
   if (lastb == 0) return ZD_E_NULL_BYTE;
   int32_t pos = (int32_t)(8 * (size - 1)) + highbit32(lastb);
-  const uint32_t G = tab[0];
-  const uint8_t* syms = (const uint8_t*)tab + DEEP_SYMS_AT;
+  const uint32_t G = tab[0] & ~DEEP_IN_POOL;
+  const uint8_t* syms = (tab[0] & DEEP_IN_POOL) ? pool + tab[DEEP_POOL_AT] : (const uint8_t*)tab + DEEP_SYMS_AT;
   const uint64_t T = 1ull << p;
   int st = 0;
   while (pos > 0 && !st) {
@@ -1326,7 +1352,8 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
                                                          const CompBlock* __restrict__ comp, CompState* cstate,
                                                          FrameState* fstate, const uint32_t* __restrict__ list,
                                                          uint32_t n_list, const uint16_t* __restrict__ luts,
-                                                         uint8_t* lits, uint32_t* k2done) {
+                                                         uint8_t* lits, uint32_t* k2done,
+                                                         const uint8_t* __restrict__ deep_pool) {
   __shared__ __attribute__((aligned(16))) uint32_t dl[K2_BLOCKS][PR_ENTRIES];
   __shared__ uint32_t counts[K2_BLOCKS][4];
   __shared__ int errs[K2_BLOCKS][4];
@@ -1379,7 +1406,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     int st;
     if (p > LUT_MAX_BITS)
       st = huf_stream_deep(blk + off, C.stream_size[k], lo, (const uint32_t*)g, p, lits + C.lit_out + start, cap,
-                           &count);
+                           &count, deep_pool);
     else if (use_lds)
       st = huf_stream_pr<const lds_u32*>(blk + off, C.stream_size[k], lo, (const lds_u32*)dl[b], L, p,
                                          lits + C.lit_out + start, cap, &count, slack);
@@ -1427,7 +1454,7 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
     const uint32_t at = redo_at[b][k];
     if (p > LUT_MAX_BITS)
       (void)huf_stream_deep(blk + off, C.stream_size[k], (uintptr_t)src, (const uint32_t*)g, p, lits + C.lit_out + at,
-                            counts[b][k], &count);
+                            counts[b][k], &count, deep_pool);
     else if (use_lds)
       (void)huf_stream_pr<const lds_u32*>(blk + off, C.stream_size[k], (uintptr_t)src, (const lds_u32*)dl[b], L, p,
                                           lits + C.lit_out + at, counts[b][k], &count,
@@ -4539,7 +4566,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        huge);
     if (huf) {                                 // the trees of more than 256 symbols the two passes listed
       hipLaunchKernelGGL(zd_k_tables_huge, dim3(K1H_GRID), dim3(K1H_LANES), 0, st, a.src, a.src_size, comp, cstate,
-                         fstate, (const uint32_t*)huge, luts);
+                         fstate, (const uint32_t*)huge, luts, (uint32_t*)(ws + W.deep));
       // K2's pair tables, from the LUTs of maxBits <= 11
       hipLaunchKernelGGL(zd_k_huf_pairs, dim3((a.n_tables + PR_WAVES - 1) / PR_WAVES), dim3(64 * PR_WAVES), 0, st,
                          comp, (const CompState*)cstate, lt, a.n_tables, luts);
@@ -4571,7 +4598,8 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (a.n_huf)
     hipLaunchKernelGGL(zd_k_huffman, dim3((a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS), dim3(K2_LANES), 0, s2, a.src, comp,
                        cstate, fstate, (const uint32_t*)(ws + W.list_huf), a.n_huf, (const uint16_t*)luts, ws + W.lits,
-                       (a.fused && fork) ? (uint32_t*)(ws + W.k2done) : (uint32_t*)nullptr);
+                       (a.fused && fork) ? (uint32_t*)(ws + W.k2done) : (uint32_t*)nullptr,
+                       (const uint8_t*)(ws + W.deep + 16));
   if (fork)
     if ((e = hipEventRecord(a.join, a.aux)) != hipSuccess) return e;
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
