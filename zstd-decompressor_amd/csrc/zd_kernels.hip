@@ -4682,14 +4682,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     const uint64_t gw = (a.j_pieces + 16 * JW_K - 1) / (16 * JW_K);   // pieces per workgroup sweep
     const uint64_t gmax = 8ull * a.cus;                              // what fits at once: 8 workgroups per CU
     const dim3 gr((uint32_t)(gw < gmax ? (gw + 7) & ~7ull : (gmax + 7) & ~7ull));   // a multiple of 8 (one eighth per XCD)
-    // rounds past the second with a smaller grid (it strides over every
-    // piece): they are the deepest chains' tail, usually empty, and an
-    // empty round then costs little more than its launch
-    const dim3 gt(std::min<uint32_t>(gr.x, 1024u));
-    // rounds 1 and 2 one launch each, the rest as one launch of sweeps
-    const uint32_t nr = a.j_rounds < 3 ? a.j_rounds : 3u;
+    // round 1 one launch, the rest as one launch of sweeps
+    // (one launch of all the sweeps: 1.43 ms for the rounds of c3s, against
+    // 1.38 with the first round launched alone; three launches, 1.38 too)
+    const uint32_t nr = a.j_rounds < 2 ? a.j_rounds : 2u;
     for (uint32_t r = 1; r <= nr; r++)
-      hipLaunchKernelGGL(zd_k_jround, r <= 2 ? gr : gt, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
+      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
                          a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == nr),
                          r == nr ? a.j_rounds - nr + 1 : 1u);
     if ((e = dom(DOM_K4J, 1)) != hipSuccess) return e;
