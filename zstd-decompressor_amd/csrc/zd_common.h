@@ -397,7 +397,8 @@ struct FrameDesc {
   uint64_t out_len0;       // bytes already produced before this launch (context API)
   uint32_t first_block;    // into BlockRec[]
   uint32_t nblocks;        // blocks to execute (0 for frames skipped by parse errors)
-  uint32_t lds;            // 1: executed by K4F (whole frame in LDS), 2: by K4J (block-parallel), 0: by the streaming K4
+  uint32_t lds;            // 1: executed by K4F (whole frame in LDS), 2: by K4J (block-parallel), 3: copied whole
+                           // by K0 (every block raw / RLE), 0: by the streaming K4
   uint32_t skip;           // leading raw/RLE blocks copied by K0 (the streaming K4 starts after them)
   uint64_t skip_bytes;     // their output bytes
 };

@@ -73,7 +73,7 @@ struct zd_plan {
   // counts of the descriptor arrays (large plans keep their descriptors only
   // in the pinned staging until the upload: the vectors above stay empty)
   uint64_t n_comps = 0, n_blocks = 0, n_frames = 0, n_tables = 0, n_huf = 0, n_seq = 0, n_k4f = 0, n_copies = 0;
-  uint64_t n_jframes = 0, n_jblk = 0, n_jseg = 0;
+  uint64_t n_jframes = 0, n_jblk = 0, n_jseg = 0, n_k0only = 0;
   bool fused = false;                           // zd_k_fused plan (build_plan fuse_plan)
   bool last_fused = false;                      // the last zd_decode_async launched zd_k_fused
   std::vector<uint64_t> frame_out, frame_cap;   // output offset and capacity per frame
@@ -438,7 +438,7 @@ void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint
 void plan_totals(zd_plan* P, const PlanCounts& T, bool fused) {
   P->n_comps = T.comps; P->n_blocks = T.blocks; P->n_frames = T.frames;
   P->n_tables = T.tables; P->n_huf = T.huf; P->n_seq = T.seq; P->n_k4f = T.k4f; P->n_copies = T.copies;
-  P->n_jframes = T.jframes; P->n_jblk = T.jblk; P->n_jseg = T.jseg;
+  P->n_jframes = T.jframes; P->n_jblk = T.jblk; P->n_jseg = T.jseg; P->n_k0only = T.k0only;
   P->fused = fused && T.jframes == 0 && T.k4f == 0;
 }
 void plan_info(zd_plan* P, const PlanCounts& T) {
@@ -1603,6 +1603,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_k4f = (uint32_t)P->n_k4f;
   a.n_copies = (uint32_t)P->n_copies;
   a.n_jframes = (uint32_t)P->n_jframes;
+  a.n_k0only = (uint32_t)P->n_k0only;
   a.n_jblk = (uint32_t)P->n_jblk;
   a.n_jseg = (uint32_t)P->n_jseg;
   // ZD_J_ROUNDS caps the rounds (a test of the path that re-plans a frame

@@ -4621,12 +4621,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                            cstate, fstate, list, n, (const uint16_t*)fses, seqs);
     }
   };
-  // the streaming K4 runs when some frame is neither K4F's nor K4J's (the
-  // others exit at once in it)
-  const bool k4_work = a.n_frames > a.n_k4f + a.n_jframes;
+  // the streaming K4 runs when some frame is not K4F's, K4J's or K0's alone
+  // (the others exit at once in it)
+  const bool k4_work = a.n_frames > a.n_k4f + a.n_jframes + a.n_k0only;
   auto k4 = [&](uint32_t f0, uint32_t f1, hipStream_t st, const uint8_t* redo) -> hipError_t {
     const uint32_t n = f1 - f0;
-    if (n && a.n_frames > a.n_k4f) {  // frames on the streaming K4 (K4F's exit at once)
+    if (n && k4_work) {  // frames on the streaming K4 (K4F's, K4J's and K0's exit at once)
       const bool tm = !redo && k4_work;
       if (tm) if ((e = dom(DOM_K4, 0)) != hipSuccess) return e;
       hipLaunchKernelGGL(zd_k_execute, dim3(n),

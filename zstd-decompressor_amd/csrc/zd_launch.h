@@ -20,6 +20,7 @@ struct LaunchArgs {
   hipStream_t aux = nullptr;   // optional second stream: K2 beside K3
   hipEvent_t fork = nullptr, join = nullptr;
   uint32_t n_jframes = 0, n_jblk = 0, n_jseg = 0;   // K4J frames / their blocks / scatter segments
+  uint32_t n_k0only = 0;                   // frames K0 copies whole (FrameDesc::lds 3)
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
   bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block

@@ -42,15 +42,16 @@ struct PlanCounts {
   uint64_t inexact = 0;          // frames whose capacity is an upper bound (no usable FCS)
   uint64_t jwords = 0;           // K4J state words: a frame's region starts a 16-word piece, 16 words of slack after
   uint64_t jpieces = 0;          // K4J 16-byte pieces over the frames' regions
+  uint64_t k0only = 0;           // frames K0 copies whole (every block raw / RLE): no K4 for them
   ZD_HD bool exact() const { return inexact == 0; }
   ZD_HD void add(const PlanCounts& o) {
     frames += o.frames; blocks += o.blocks; comps += o.comps; luts += o.luts; fses += o.fses; lits += o.lits;
     nrec += o.nrec; nseq += o.nseq; out += o.out; tables += o.tables; huf += o.huf; seq += o.seq; k4f += o.k4f;
     copies += o.copies; jframes += o.jframes; jblk += o.jblk; jseg += o.jseg; inexact += o.inexact;
-    jwords += o.jwords; jpieces += o.jpieces;
+    jwords += o.jwords; jpieces += o.jpieces; k0only += o.k0only;
   }
 };
-constexpr int PLAN_FIELDS = 20;
+constexpr int PLAN_FIELDS = 21;
 static_assert(sizeof(PlanCounts) == PLAN_FIELDS * 8, "PlanCounts: u64 fields only");
 
 // Plan-wide inputs of the per-frame pass.  `prev_*` seed the Treeless/Repeat
@@ -291,6 +292,13 @@ ZD_HD void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hb
     }
     fd.skip = k;
     fd.skip_bytes = pre;
+    // every block copied by K0: the frame's length is known here, and no
+    // executor runs it (a launch less when no frame needs the streaming K4)
+    if (k == fd.nblocks && fs.key == KEY_NONE) {
+      fd.lds = 3;
+      fs.out_len = X.out_len0 + pre;
+      c.k0only++;
+    }
   }
   if (FILL) {
     S.frame_out[fi] = c.out;
