@@ -159,12 +159,12 @@ def c2_raw_rle(total: int = 64 << 20, block: int = 128 << 10, seed: int = SEED +
 
 
 def frames(data: bytes, chunk: int, level: int = 3, threads: int | None = None,
-           checksum: bool = False, window_log: int = 0) -> bytes:
+           checksum: bool = False, window_log: int = 0, content_size: bool = True) -> bytes:
     """Independent frames of `chunk` decompressed bytes each (last may be short)."""
     parts = [data[i:i + chunk] for i in range(0, len(data), chunk)]
     threads = threads or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(threads) as ex:
-        out = list(ex.map(lambda p: libzstd.compress(p, level, checksum, window_log), parts))
+        out = list(ex.map(lambda p: libzstd.compress(p, level, checksum, window_log, content_size), parts))
     return b"".join(out)
 
 

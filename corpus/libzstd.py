@@ -77,8 +77,11 @@ def _chk(r):
     return r
 
 
-def compress(data: bytes, level: int = 3, checksum: bool = False, window_log: int = 0) -> bytes:
-    """One frame.  ctypes drops the GIL, so threads compress in parallel."""
+def compress(data: bytes, level: int = 3, checksum: bool = False, window_log: int = 0,
+             content_size: bool = True) -> bytes:
+    """One frame (content_size False: no Frame_Content_Size field, as a
+    streaming compressor writes).  ctypes drops the GIL, so threads compress
+    in parallel."""
     L = lib()
     cap = L.ZSTD_compressBound(len(data))
     dst = C.create_string_buffer(cap)
@@ -88,6 +91,8 @@ def compress(data: bytes, level: int = 3, checksum: bool = False, window_log: in
         _chk(L.ZSTD_CCtx_setParameter(cctx, ZSTD_c_checksumFlag, int(checksum)))
         if window_log:
             _chk(L.ZSTD_CCtx_setParameter(cctx, ZSTD_c_windowLog, window_log))
+        if not content_size:
+            _chk(L.ZSTD_CCtx_setParameter(cctx, ZSTD_c_contentSizeFlag, 0))
         n = _chk(L.ZSTD_compress2(cctx, dst, cap, data, len(data)))
     finally:
         L.ZSTD_freeCCtx(cctx)

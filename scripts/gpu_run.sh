@@ -36,6 +36,8 @@ for s in "$@"; do
     c3var:*) v=${s#c3var:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run bench_c3_$v 600 python bench.py --workload c3 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
     c2bigvar:*) v=${s#c2bigvar:}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c2big_$v 600 python bench.py --workload c2 --c2-mib 1024 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
     c2var:*) v=${s#c2var:}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c2_$v 600 python bench.py --workload c2 --steps 20 --warmup 5 --no-cpu-baseline --no-host-io ;;
+    nofcs) run time_no_fcs 600 python -u scripts/time_no_fcs.py ;;
+    nofcsvar:*) v=${s#nofcsvar:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run time_no_fcs_$v 600 python -u scripts/time_no_fcs.py ;;
     benchc3) run bench_c3 600 python bench.py --workload c3 --steps 5 --warmup 2 --no-cpu-baseline ;;
     nofarq) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_nofar.so run bench_nofar 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-verify --experiment --no-host-io ;;
     k3q8q) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_k3q8.so run bench_k3q8 600 python bench.py --steps 3 --warmup 1 --unique-mib 256 --replicas 4 --no-cpu-baseline --no-host-io ;;

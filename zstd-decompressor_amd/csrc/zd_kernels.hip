@@ -4513,13 +4513,27 @@ hipError_t launch_xxh64(const uint8_t* base, const uint64_t* d_off, const uint64
 // ---------------------------------------------------------------------------
 // compaction (frames without an exact FCS layout)
 // ---------------------------------------------------------------------------
+// One frame per blockIdx.x, COMPACT_SPLIT workgroups (blockIdx.y) over
+// its bytes: 16-byte loads and aligned 16-byte stores, head and tail bytewise
+// (as K0: more workgroups with less work each keep more copies in flight).
+constexpr uint32_t COMPACT_SPLIT = 8;
 __global__ __launch_bounds__(256) void zd_k_compact(const uint8_t* __restrict__ staging, uint8_t* dst,
                                                     const uint64_t* from, const uint64_t* to, const uint64_t* len) {
   const uint32_t f = blockIdx.x;
   const uint8_t* s = staging + from[f];
   uint8_t* d = dst + to[f];
   const uint64_t n = len[f];
-  for (uint64_t x = threadIdx.x; x < n; x += blockDim.x) d[x] = s[x];
+  const uint64_t head = min(n, (uint64_t)((16 - ((uintptr_t)d & 15)) & 15));
+  const uint64_t nch = (n - head) / 16;                       // whole 16-byte chunks after the head
+  const uint64_t per = (nch + COMPACT_SPLIT - 1) / COMPACT_SPLIT;
+  const uint64_t c0 = per * blockIdx.y, c1 = min(nch, c0 + per);
+  for (uint64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x)
+    *(g_u32x4*)(d + head + 16 * c) = ldg16(s + head + 16 * c);
+  if (blockIdx.y == 0) {
+    if (threadIdx.x < head) d[threadIdx.x] = s[threadIdx.x];
+    const uint64_t tail0 = head + 16 * nch;
+    if (tail0 + threadIdx.x < n) d[tail0 + threadIdx.x] = s[tail0 + threadIdx.x];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -4728,7 +4742,7 @@ namespace zd {
 hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* d_from, const uint64_t* d_to,
                           const uint64_t* d_len, uint32_t n, hipStream_t s) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(zd_k_compact, dim3(n), dim3(256), 0, s, staging, dst, d_from, d_to, d_len);
+  hipLaunchKernelGGL(zd_k_compact, dim3(n, COMPACT_SPLIT), dim3(256), 0, s, staging, dst, d_from, d_to, d_len);
   return hipGetLastError();
 }
 
