@@ -2653,32 +2653,6 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         // off32: a fresh lane's offset (offset_value - 3; 2^32 - 1 for the
         // context API's giant values), a repeat lane's once the walk set it
         uint32_t off32 = giant ? 0xFFFFFFFFu : ofv - 3;
-        // matches whose source lies wholly in HBM, flushed two batches ago or
-        // earlier (those stores completed before this batch's waits): their
-        // first 32 source bytes are loaded early, to land during the checks
-        // and the literal copies -- a fresh lane's before the repeat walk
-        // (its offset is known), a repeat lane's after it
-        const int32_t q = X.pos + (int32_t)(opos + ll);
-        const int32_t fl_lim = X.hs < fl_safe ? X.hs : fl_safe;
-        auto far_of = [&](uint32_t o) -> bool {
-          const int32_t sl = q - (int32_t)o;
-          return valid && lane < kk && ml && o >= 16 && o <= (uint32_t)q && sl + (int32_t)(o < ml ? o : ml) <= fl_lim;
-        };
-#if ZD_K4_OVS
-        // pass 0 (below) writes each lane's sequence as 16-byte chunks that
-        // merge its literal and match bytes; a far lane's first two chunks'
-        // match bytes are loaded early (chunk b reads the source at
-        // slo + b - ll, so the match bytes land at chunk offset ll - b; a
-        // chunk of literal bytes only reads at slo)
-        u32x4 fv0, fv1;
-        const uint32_t n0f = ll + ml;
-        const uint32_t bb1 = n0f >= 32 ? 16u : (n0f > 16 ? n0f - 16 : 0u);
-        auto far_loads = [&](int32_t sl) {
-          fv0 = ldg16_src(X.out + (uint32_t)(ll >= 16 ? sl : sl - (int32_t)ll));
-          if (n0f > 16) fv1 = ldg16_src(X.out + (uint32_t)(ll >= bb1 + 16 ? sl : sl + (int32_t)bb1 - (int32_t)ll));
-        };
-        if (fresh && far_of(off32) && q - (int32_t)off32 >= 16) far_loads(q - (int32_t)off32);
-#endif
         int derr = 0;
         uint64_t rm = __ballot(valid && !fresh && lane < kk);
         // state after lane `prev` (uniform: readfirstlane keeps the walk on the scalar unit)
@@ -2727,12 +2701,29 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
           rep[0] = b0; rep[1] = b1; rep[2] = b2;
         };
         K4_PHASE(1);
+        // matches whose source lies wholly in HBM, flushed two batches ago or
+        // earlier (those stores completed before this batch's waits): their
+        // first 32 source bytes are loaded now, to land during the checks
+        // and the literal copies
+        const int32_t q = X.pos + (int32_t)(opos + ll);
         const int32_t slo = q - (int32_t)off32;
         const int32_t shi = slo + (int32_t)(off32 < ml ? off32 : ml);
-        const bool far = far_of(off32);
+        const bool far = valid && lane < kk && ml && off32 >= 16 && off32 <= (uint32_t)q &&
+                         shi <= (X.hs < fl_safe ? X.hs : fl_safe);
 #if ZD_K4_OVS
+        // pass 0 (below) writes each lane's sequence as 16-byte chunks that
+        // merge its literal and match bytes; a far lane's first two chunks'
+        // match bytes are loaded now (chunk b reads the source at slo + b - ll,
+        // so the match bytes land at chunk offset ll - b; a chunk of literal
+        // bytes only reads at slo)
+        u32x4 fv0, fv1;
         const bool far0 = far && slo >= 16;
-        if (far0 && !fresh) far_loads(slo);
+        const uint32_t n0f = ll + ml;
+        const uint32_t bb1 = n0f >= 32 ? 16u : (n0f > 16 ? n0f - 16 : 0u);
+        if (far0) {
+          fv0 = ldg16_src(X.out + (uint32_t)(ll >= 16 ? slo : slo - (int32_t)ll));
+          if (n0f > 16) fv1 = ldg16_src(X.out + (uint32_t)(ll >= bb1 + 16 ? slo : slo + (int32_t)bb1 - (int32_t)ll));
+        }
 #else
         u32x4 fv0, fv1;
         if (far) {
