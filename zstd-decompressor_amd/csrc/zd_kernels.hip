@@ -2091,11 +2091,16 @@ __device__ inline uint64_t rec_lane(uint64_t raw, int lane) {
 // source period by period, byte q+j = byte q-off+(j mod off), which is the
 // reference's byte-by-byte push (decoding_context.rs:95-98).
 // ---------------------------------------------------------------------------
+// History and room of the 7,200-byte window (round 5, C4 10 GiB on one box:
+// history 1 / 2 / 3 / 4 / 4.5 / 5 / 5.25 KiB -> K4 18.70 / 18.23 / 17.98 /
+// 17.66 / 17.73 / 18.74 / 18.71 ms -- more matches find their source in LDS
+// until the slides come every batch; room 1792 / 1536 / 1280 at 4 KiB:
+// 17.72 / 17.69 / 17.62, within noise)
 #ifndef ZD_K4_W
-#define ZD_K4_W 2048
+#define ZD_K4_W 4096
 #endif
 #ifndef ZD_K4_B
-#define ZD_K4_B 1792
+#define ZD_K4_B 1536
 #endif
 constexpr int K4_W = ZD_K4_W;                 // history kept after a slide
 constexpr int K4_B = ZD_K4_B;                 // room kept for a batch (a slide when less is left)
