@@ -1612,10 +1612,11 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.j_rounds = rounds_env && P->j_rounds ? std::min<uint32_t>(P->j_rounds, (uint32_t)std::max(1, atoi(rounds_env)))
                                          : P->j_rounds;
   a.j_pieces = P->j_pieces;
-  // hops per pending word and K4J round (c3s, scripts/exp_jhops.sh: 1 hop
-  // 10.2 ms, 2 5.2, 4 3.0, 8 2.44, 16 2.67, 32 2.95); ZD_J_HOPS overrides
+  // hops per pending word and K4J round (c3s, scripts/exp_jhops.sh, K4J ms
+  // with the word-per-lane rounds, round 5: 4 hops 1.91, 5 1.85, 6 1.75-1.77,
+  // 7 1.76, 8 1.78-1.79, 12 1.85, 16 1.90); ZD_J_HOPS overrides
   static const char* hops_env = getenv("ZD_J_HOPS");
-  a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 8u;
+  a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 6u;
   a.cus = (uint32_t)(k3_slots() / 64);
   a.stream = s;
   // K3 as four lanes per block (K3Q, default): C3 (763 blocks) 2.89 -> 2.31

@@ -3815,7 +3815,7 @@ __global__ __launch_bounds__(K4F_T) void zd_k_execute_lds(const uint8_t* __restr
 //                     passed in an overlapping match: the reference's
 //                     byte-by-byte push)
 //   KJ4 zd_k_jround   pointer jumping, in place: S[p] = S[p - S[p]] for every
-//                     pending word, up to 8 hops per word and round (a final
+//                     pending word, up to j_hops (6) hops per word and round (a final
 //                     source hands over its byte, a pending one adds its
 //                     distance), one word per lane.
 //                     A chain ends at a literal after at most one hop per
