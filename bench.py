@@ -270,8 +270,57 @@ def traffic_commit():
         return None
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, n: int, port: int):
+    """The command and environment that run this bench as `n` ranks, one
+    process per GPU (torch.distributed.run on 127.0.0.1), with the same
+    arguments.  The children see WORLD_SIZE and take the rank path."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # RCCL needs dmabuf IPC on these hosts
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return cmd, env
+
+
+def maybe_launch(argv) -> int | None:
+    """`--gpus N` (N > 1) without a launcher: start the N ranks as ONE child
+    process group (torchrun) before anything touches the GPU, forward their
+    output (rank 0 prints the JSON line) and return their exit code.  Under
+    a launcher (WORLD_SIZE set) return None and check WORLD_SIZE == N."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run-launch", action="store_true")
+    a, _ = ap.parse_known_args(argv)
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        assert int(world) == a.gpus or a.gpus == 1 and "--gpus" not in " ".join(argv), \
+            f"WORLD_SIZE={world} but --gpus {a.gpus}"
+        return None
+    if a.gpus <= 1:
+        return None
+    fwd = [x for x in argv if x != "--dry-run-launch"]
+    cmd, env = launch_command(fwd, a.gpus, free_port())
+    if a.dry_run_launch:
+        print(json.dumps({"cmd": cmd, "env": {k: env[k] for k in ("HSA_ENABLE_IPC_MODE_LEGACY", "OMP_NUM_THREADS")}}))
+        return 0
+    import subprocess
+    log(f"[launch] {a.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
+    rc = maybe_launch(sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     ap = argparse.ArgumentParser()
+    ap.add_argument("--dry-run-launch", action="store_true", help="N>1: print the rank launch command and exit")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
