@@ -159,6 +159,10 @@ typedef struct zd_plan zd_plan;
  * runs one wave per block by default; this flag keeps K1's serial lanes.
  * Same tables either way; tests run both. */
 #define ZD_F_K1_LANES     64u
+/* Test switch: K4J runs ONE pointer-jumping round of one hop, so a frame
+ * whose match chains are deeper keys LS_JROUNDS and zd_plan_decompress plans
+ * it again on the streaming executor (tests/test_large_frames.py). */
+#define ZD_F_J_ONE_ROUND 128u
 
 /* zd_plan_info.executors: */
 #define ZD_EXEC_FUSED 1u   /* zd_k_fused: tables, FSE chains and execution per group of four

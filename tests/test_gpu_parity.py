@@ -78,6 +78,9 @@ def test_execute_sequences_large_values():
         [(150_000, 140_000 + 3, 140_000), (1, 1, 270_000), (70_000, 3, 5)],       # long copies, repeat codes
         [(10, (1 << 29) + 10, 4)],                                 # an offset past the output: ImpossibleValue
         [(262_144, 200_000 + 3, 1 << 18), (0, (1 << 31) + 7, 3)],  # a giant offset after a long run
+        [(20, 4, 1), (0xFFFFFFF0, 4, 1)],                          # 20 + ll wraps 32 bits: ImpossibleValue
+        [(0xFFFFFFFF, 4, 1)],                                      # the largest literals_length
+        [(5, 4, 1)] * 63 + [(0xFFFFFFF0, 4, 1)] * 3 + [(1, 4, 1)], # wrapping lanes inside one batch
     ]
     for i, seqs in enumerate(cases):
         try:
@@ -156,9 +159,12 @@ def test_synthetic_multi_block_frames(kind, level):
     assert ost == 0
 
 
-def test_c2_raw_rle():
-    data = gen.c2_raw_rle(8 << 20)
-    ost, gst = assert_parity(data, False, "c2")
+@pytest.mark.parametrize("mib", [8, 64])
+def test_c2_raw_rle(mib):
+    """C2 (BASELINE configs[1]): one raw/RLE-only frame; 64 MiB is the bench
+    size (K0 copies the frame whole)."""
+    data = gen.c2_raw_rle(mib << 20)
+    ost, gst = assert_parity(data, False, f"c2 {mib} MiB")
     assert ost == 0
 
 
@@ -687,6 +693,79 @@ def test_k2_tree_past_the_lut_slot():
         parts.append(ok[i % len(ok)] if i % 2 else gen.frames(src[i * 12_000:(i + 1) * 12_000], 12_000, 3))
     ost, _ = assert_parity(b"".join(parts), False, "trees of 7,709 leaves inside libzstd frames")
     assert ost == 0
+
+
+def _tree_codes_7709():
+    _, widths = oracle.huffman_widths(DEEP_DESC_7709)
+    p = max(widths)
+    codes, pos = {}, 0
+    for w in range(p, 0, -1):
+        S = 1 << (p - w)
+        al = (pos + S - 1) & ~(S - 1)
+        for i in (i for i, x in enumerate(widths) if x == w):
+            if al + S > 1 << p:
+                break
+            codes[i] = (al >> (p - w), w)
+            al += S
+        pos = al
+    return codes
+
+
+def _tree_block(r, codes, n, treeless, last, seqbits):
+    """One compressed block: n literals under DEEP_DESC_7709's tree (its
+    description in the block, or Treeless: the previous block's tree,
+    literals.rs:88-206 type 3), then one sequence of the given bits."""
+    keys = list(codes)
+    v = 1
+    for _ in range(n):
+        c, w = codes[r.choice(keys)]
+        v = (v << w) | c
+    stream = v.to_bytes((v.bit_length() + 7) // 8, "little")
+    desc = b"" if treeless else DEEP_DESC_7709
+    comp = len(desc) + len(stream)
+    lh = ((3 if treeless else 2) | (0 << 2) | (n << 4) | (comp << 14)).to_bytes(3, "little")
+    content = lh + desc + stream + bytes([1, 0x00]) + seqbits
+    return ((len(content) << 3) | (2 << 1) | int(last)).to_bytes(3, "little") + content
+
+
+def test_context_deep_pool_tree_then_treeless():
+    """Block.decode(ctx) of a block whose tree keeps its symbols in the plan's
+    deep pool (7,709 leaves), then Treeless blocks reusing that tree: the
+    context persists the pool with the LUT slot (block.rs:74-99 through one
+    DecodingContext), against the oracle's decode of the same frame and the
+    batch path's."""
+    from zstd_decompressor import ForwardByteParser, Block, DecodingContext, MAX_WIN_SIZE
+    codes = _tree_codes_7709()
+    r = random.Random(57)
+    head = b"\x28\xb5\x2f\xfd" + bytes([0x00, 0x50])
+    for trial in range(2):
+        blocks = []
+        for k in range(3):
+            # the block's sequence: random bits until the frame so far decodes
+            for attempt in range(2000):
+                n = r.randrange(100, 400)
+                seed = r.randrange(1 << 30)
+                bits = bytes(random.Random(seed).randrange(256) for _ in range(4)) + bytes([r.randrange(1, 256)])
+                cand = _tree_block(random.Random(seed), codes, n, k > 0, True, bits)
+                if oracle.decompress_status(head + b"".join(blocks) + cand, False)[0] == 0:
+                    blocks.append(_tree_block(random.Random(seed), codes, n, k > 0, k == 2, bits))
+                    break
+            else:
+                pytest.fail(f"no decodable sequence for block {k}")
+        frame = head + b"".join(blocks)
+        ost, expect = oracle.decompress_status(frame, False)
+        assert ost == 0
+        assert_parity(frame, False, f"deep tree + Treeless #{trial}")
+        p = ForwardByteParser(frame)
+        p.slice(6)
+        ctx = DecodingContext(MAX_WIN_SIZE)
+        while True:
+            b, last = Block.parse(p)
+            b.decode(ctx)
+            if last:
+                break
+        assert ctx.decoded == expect, f"trial {trial}: context output differs"
+        ctx.close()
 
 def _pair_table_kind(weights):
     """Which pair-table entries a tree of direct weights gives K2

@@ -159,7 +159,7 @@ tile = gen.text(4096, seed=15)
 src = b"".join(bytes([i & 255]) + tile for i in range(1200))      # every tile copies the one before
 for s in (src, gen.text(3_000_000, seed=16)):
     data = libzstd.compress(s, 3)
-    p = Plan(data, False, _lib.F_BLOCK_PARALLEL)
+    p = Plan(data, False, _lib.F_BLOCK_PARALLEL | _lib.F_J_ONE_ROUND)
     pp, n, keep = _lib.buf(data)
     st, out = run_plan(p, pp, n)
     print(st, int(out == s), p.refresh_info().replans, flush=True)
@@ -168,18 +168,18 @@ for s in (src, gen.text(3_000_000, seed=16)):
 
 
 def test_block_parallel_unconverged_replans(tmp_path):
-    """K4J with its pointer jumping cut to one round of one hop (ZD_J_ROUNDS,
-    ZD_J_HOPS: the rounds' last sweep finds pending pieces): the frame keys
-    LS_JROUNDS and zd_plan_decompress plans it again on the streaming
-    executor -- same bytes, one re-plan.  In a child process (the knobs are
-    read once per process)."""
+    """K4J with its pointer jumping cut to one round of one hop (the plan's
+    test switch ZD_F_J_ONE_ROUND: the rounds' last sweep finds pending
+    pieces): the frame keys LS_JROUNDS and zd_plan_decompress plans it again
+    on the streaming executor -- same bytes, one re-plan.  In a child
+    process."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     script = tmp_path / "unconverged.py"
     script.write_text(_UNCONVERGED)
-    env = dict(os.environ, ZD_J_ROUNDS="1", ZD_J_HOPS="1")
+    env = dict(os.environ)
     r = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l.split() for l in r.stdout.strip().splitlines()]

@@ -424,7 +424,16 @@ void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint
   if (T.jframes) {
     uint32_t r = 1;
     while (r < (uint32_t)J_MAX_ROUNDS - 1 && (1ull << r) <= j_maxseq + 1) r++;
-    P->j_rounds = r + 1;
+    // a hop whose composed distance would reach 2^31 (J_FINAL) keeps its
+    // word until its source is final, so a chain spanning k windows of
+    // 2 GiB resolves within k times the rounds of one (by induction on k:
+    // the bytes of the windows below are final by then, and the rest of
+    // the chain is one window of hops ending at them); j_base (the plan's
+    // K4J words) bounds the largest frame.  Rounds past the first are
+    // sweeps that stop when nothing is pending: the bound costs nothing
+    // on frames that converge sooner.
+    const uint64_t k = std::max<uint64_t>(1, (j_base + (1ull << 31) - 1) >> 31);
+    P->j_rounds = (uint32_t)((r + 1) * k);
   }
   W.jblk = carve(sizeof(JBlk) * std::max<uint64_t>(T.jblk, 1));
   W.jseg = carve(sizeof(JSeg) * std::max<uint64_t>(T.jseg, 1));
@@ -1606,17 +1615,17 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   a.n_k0only = (uint32_t)P->n_k0only;
   a.n_jblk = (uint32_t)P->n_jblk;
   a.n_jseg = (uint32_t)P->n_jseg;
-  // ZD_J_ROUNDS caps the rounds (a test of the path that re-plans a frame
-  // whose pointer jumping did not converge on the streaming executor)
-  static const char* rounds_env = getenv("ZD_J_ROUNDS");
-  a.j_rounds = rounds_env && P->j_rounds ? std::min<uint32_t>(P->j_rounds, (uint32_t)std::max(1, atoi(rounds_env)))
-                                         : P->j_rounds;
+  // ZD_F_J_ONE_ROUND (a test switch, set per plan) cuts the rounds to one
+  // of one hop: the path that re-plans a frame whose pointer jumping did not
+  // converge, on the streaming executor
+  const bool one_round = (P->flags & ZD_F_J_ONE_ROUND) != 0;
+  a.j_rounds = one_round && P->j_rounds ? 1u : P->j_rounds;
   a.j_pieces = P->j_pieces;
   // hops per pending word and K4J round (c3s, scripts/exp_jhops.sh, K4J ms
   // with the word-per-lane rounds, round 5: 4 hops 1.91, 5 1.85, 6 1.75-1.77,
   // 7 1.76, 8 1.78-1.79, 12 1.85, 16 1.90); ZD_J_HOPS overrides
   static const char* hops_env = getenv("ZD_J_HOPS");
-  a.j_hops = hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 6u;
+  a.j_hops = one_round ? 1u : hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 6u;
   a.cus = (uint32_t)(k3_slots() / 64);
   a.stream = s;
   // K3 as four lanes per block (K3Q, default): C3 (763 blocks) 2.89 -> 2.31
@@ -1981,6 +1990,11 @@ struct zd_context {
   uint8_t al[3] = {0, 0, 0};
   bool has_huf = false;
   bool has_tab[3] = {false, false, false};
+  // the persisted Huffman table's deep-tree pool (a tree with more leaves
+  // than a LUT slot holds keeps its symbols there): the pool's counter and
+  // bytes as the plan that built it left them, deep_used bytes
+  uint8_t* d_deep = nullptr;
+  uint32_t deep_used = 0;
   // kept between calls: the stream every block runs on (one synchronisation
   // per block) and the block-input buffer (grown, never freed per call)
   hipStream_t s = nullptr;
@@ -2040,6 +2054,7 @@ void zd_context_free(zd_context* c) {
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_fse) (void)hipFree(c->d_fse);
+  if (c->d_deep) (void)hipFree(c->d_deep);
   if (c->d_in) (void)hipFree(c->d_in);
   if (c->s) { (void)hipStreamSynchronize(c->s); (void)hipStreamDestroy(c->s); }
   delete c;
@@ -2080,6 +2095,11 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
     pcs.huf_bits = c->huf_bits;
     for (int k = 0; k < 3; k++) pcs.al[k] = c->al[k];
     HIPCHK(hipMemcpyAsync(P->d_ws + P->W.comp_state, &pcs, sizeof pcs, hipMemcpyHostToDevice, s));
+    // a Treeless block reuses the persisted tree: when its symbols live in
+    // the deep pool, the pool comes back too, at the offsets the LUT slot's
+    // DEEP_POOL_AT word names (its counter included, so nothing new lands on it)
+    if (P->comps.size() > 1 && P->comps[1].lit_type == LIT_TREELESS && c->has_huf && c->deep_used)
+      HIPCHK(hipMemcpyAsync(P->d_ws + P->W.deep, c->d_deep, 16 + (size_t)c->deep_used, hipMemcpyDeviceToDevice, s));
   }
   P->info.out_exact = 1;    // output goes straight into the context buffer
   P->fdesc[0].out = 0;
@@ -2099,7 +2119,9 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
   const size_t nc = P->comps.size();
   std::vector<CompState> cst(std::max<size_t>(nc, 1));
   FrameState st{};
+  uint32_t deep_used = 0;
   HIPCHK(hipMemcpyAsync(&st, P->d_ws + P->W.frame_state, sizeof st, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&deep_used, P->d_ws + P->W.deep, 4, hipMemcpyDeviceToHost, s));
   if (nc) HIPCHK(hipMemcpyAsync(cst.data(), P->d_ws + P->W.comp_state, nc * sizeof(CompState), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   int code = key_code(st.key);
@@ -2117,6 +2139,16 @@ static int ctx_run(zd_context* c, zd_plan* P, const uint8_t* src, size_t n) {
                             hipMemcpyDeviceToDevice, s));
       c->huf_bits = cs.huf_bits;
       c->has_huf = true;
+      c->deep_used = 0;
+      if (deep_used) {             // the new tree's symbols are in the plan's pool
+        if (!c->d_deep && hipMalloc(&c->d_deep, 16 + (size_t)DEEP_POOL_BYTES) != hipSuccess) {
+          c->d_deep = nullptr;
+          c->has_huf = false;
+          return ZD_E_NO_MEMORY;
+        }
+        HIPCHK(hipMemcpyAsync(c->d_deep, P->d_ws + P->W.deep, 16 + (size_t)deep_used, hipMemcpyDeviceToDevice, s));
+        c->deep_used = deep_used;
+      }
     }
     for (int k = 0; k < 3 && cb.nseq; k++) {
       int32_t srcc = cb.tab_src[k];
@@ -2302,10 +2334,16 @@ int zd_execute_sequences(zd_context* c, const uint32_t* ll, const uint32_t* ofv,
   std::vector<DirectSide> side;
   if (nseq) {
     for (size_t i = 0; i < nseq; i++) {
-      const bool esc = ll[i] >= 0x1FFFF || ml[i] >= 0x3FFFF || ofv[i] >= DIRECT_GIANT;
+      // K4's literal and offset checks run in 32 bits; a literals_length
+      // past every literal the block holds is ImpossibleValue whatever its
+      // size (decoding_context.rs:86-90), so it is clamped to nlits + 1:
+      // the outcome is the reference's and no batch sum can wrap (nlits and
+      // every match length are below K4_MAX_FRAME_OUT < 2^31)
+      const uint32_t lli = (uint32_t)std::min<uint64_t>(ll[i], (uint64_t)nlits + 1);
+      const bool esc = lli >= 0x1FFFF || ml[i] >= 0x3FFFF || ofv[i] >= DIRECT_GIANT;
       if (esc && side.empty()) side.assign(nseq, DirectSide{});
-      if (esc) side[i] = DirectSide{ll[i], ml[i], ofv[i], 0};
-      rec[i] = esc ? DIRECT_ESCAPE : seq_pack(ll[i], ml[i], ofv[i]);
+      if (esc) side[i] = DirectSide{lli, ml[i], ofv[i], 0};
+      rec[i] = esc ? DIRECT_ESCAPE : seq_pack(lli, ml[i], ofv[i]);
     }
     if (!side.empty()) {
       if (hipMalloc(&d_side, side.size() * sizeof(DirectSide)) != hipSuccess) { d_side = nullptr; return fin(ZD_E_NO_MEMORY); }

@@ -2503,6 +2503,13 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
 #else
 #define K4_PHASE(i) do { } while (0)
 #endif
+// ISA markers (tests/test_isa_pass0.py compiles with -DZD_ISA_MARKS=1 and
+// checks the instructions between them): empty in the library
+#if ZD_ISA_MARKS
+#define ZD_ISA_MARK(txt) asm volatile(txt)
+#else
+#define ZD_ISA_MARK(txt) do { } while (0)
+#endif
 
   for (uint32_t j = F.skip; j < F.nblocks && err_key == KEY_NONE; j++) {
     const BlockRec B = blocks[F.first_block + j];
@@ -2812,7 +2819,9 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
             v.y = ((uint32_t)(mlo >> 32) & lv.y) | (~(uint32_t)(mlo >> 32) & mv.y);
             v.z = ((uint32_t)mhi & lv.z) | (~(uint32_t)mhi & mv.z);
             v.w = ((uint32_t)(mhi >> 32) & lv.w) | (~(uint32_t)(mhi >> 32) & mv.w);
-            *(l_u32x4a1*)(d + bb) = v;
+            ZD_ISA_MARK("; ZDPUT<");
+            *(l_u32x4a1*)(d + bb) = v;       // ONE ds_write_b128 (test_isa_pass0)
+            ZD_ISA_MARK("; ZDPUT>");
           };
           auto mload = [&](uint32_t bb) -> u32x4 {
             return src_far ? ldg16_src(X.out + (uint32_t)msrc(bb)) : src_win ? lds16(X.at(msrc(bb))) : f4;
