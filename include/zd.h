@@ -159,6 +159,10 @@ typedef struct zd_plan zd_plan;
  * runs one wave per block by default; this flag keeps K1's serial lanes.
  * Same tables either way; tests run both. */
 #define ZD_F_K1_LANES     64u
+/* Sequence-decode choice for plans of few blocks (<= 8 per CU): K3 runs
+ * one block per wave (zd_k_sequences_l, latency-first) by default; this flag
+ * keeps K3Q.  Same records either way; tests run both. */
+#define ZD_F_SEQ_NO_LATENCY 256u
 /* Test switch: K4J runs ONE pointer-jumping round of one hop, so a frame
  * whose match chains are deeper keys LS_JROUNDS and zd_plan_decompress plans
  * it again on the streaming executor (tests/test_large_frames.py). */

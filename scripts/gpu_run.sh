@@ -33,6 +33,8 @@ for s in "$@"; do
     profc3svar:*) v=${s#profc3svar:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run prof_c3s_$v 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3s_$v -o run --output-format csv -- python bench.py --workload c3s --steps 3 --warmup 1 --no-cpu-baseline --no-host-io ;;
     pmcj) run pmc_j1 300 rocprofv3 --kernel-trace --kernel-include-regex "zd_k_jround|zd_k_jscatter" --pmc SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU -d gpurun_out/pmc_j1 -o run --output-format csv -- python bench.py --workload c3s --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io && run pmc_j2 300 rocprofv3 --kernel-trace --kernel-include-regex "zd_k_jround|zd_k_jscatter" --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum -d gpurun_out/pmc_j2 -o run --output-format csv -- python bench.py --workload c3s --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host-io ;;
     c3senv:*) e=${s#c3senv:}; run bench_c3s_env_${e//[=,]/_} 600 env ${e//,/ } python bench.py --workload c3s --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
+    fztrace) ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_fztrace.so run fztrace 300 python scripts/fztrace.py ;;
+    c3env:*) e=${s#c3env:}; run bench_c3_env_${e//[=,]/_} 600 env ${e//,/ } python bench.py --workload c3 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
     c3var:*) v=${s#c3var:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run bench_c3_$v 600 python bench.py --workload c3 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
     c2bigvar:*) v=${s#c2bigvar:}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c2big_$v 600 python bench.py --workload c2 --c2-mib 1024 --steps 10 --warmup 3 --no-cpu-baseline --no-host-io ;;
     c2var:*) v=${s#c2var:}; if [ "$v" = base ]; then lib=zstd-decompressor_amd/lib/libzd.so; else lib=zstd-decompressor_amd/lib/variants/libzd_$v.so; fi; ZD_LIB_PATH=$lib run bench_c2_$v 600 python bench.py --workload c2 --steps 20 --warmup 5 --no-cpu-baseline --no-host-io ;;
@@ -66,6 +68,7 @@ for s in "$@"; do
     ovlp:*) n=${s#ovlp:}; run bench_ovlp_$n 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io --overlap-streams $n ;;
     titer) run pytest_iter 300 python -u -m pytest -x -v -p no:cacheprovider --timeout 120 --timeout-method thread -m gpu tests/test_frame_iterator.py tests/test_lds_order.py ;;
     ldsorder) run lds_order 120 tools/lds_order_check 4096 256 ;;
+    salub) run salu_bench 120 tools/salu_bench ;;
     testshard) run pytest_shard 600 python -u -m pytest -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu tests/test_shard.py ;;
     env:*) e=${s#env:}; run bench_env_${e//[=,]/_} 600 env ${e//,/ } python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;
     var:*) v=${s#var:}; ZD_LIB_PATH=zstd-decompressor_amd/lib/variants/libzd_$v.so run bench_var_$v 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-io ;;

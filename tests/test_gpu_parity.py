@@ -299,16 +299,20 @@ def test_many_frame_roundtrip_large():
 
 
 def test_one_lane_k3_chain(resources):
-    """K3 runs four lanes per block by default (K3Q, seq_chainq); the plan flag
-    ZD_F_SEQ_ONE_LANE keeps the one-lane chain (seq_chainfl).  Both against
-    the oracle: the resources, multi-block frames and corruptions inside a
-    300-frame plan."""
+    """K3's three chains (sequences.rs:191-237): K3Q, four lanes per block
+    (seq_chainq; ZD_F_SEQ_NO_LATENCY forces it in plans of few blocks); K3L,
+    one block per wave (seq_chainl, the default in plans of <= 8 blocks per
+    CU); the one-lane chain (ZD_F_SEQ_ONE_LANE, seq_chainfl).  All against
+    the oracle: the resources, multi-block frames, L19 binary (long offset
+    codes) and corruptions inside a 300-frame plan."""
     from zstd_decompressor import _lib
     r = random.Random(79)
     src = gen.text(300 * 4096, seed=15)
     base = gen.frames(src, 4096, 3)
     multi = gen.frames(gen.text(2 << 20, seed=16), 1 << 20, 9)
-    for flags in (_lib.F_SEQ_ONE_LANE, 0):
+    binl19 = gen.frames(gen.binary(1 << 20, seed=17), 128 << 10, 19)
+    for flags in (_lib.F_SEQ_ONE_LANE, _lib.F_SEQ_NO_LATENCY, 0):
+        assert_parity(binl19, False, f"flags={flags} binary L19", flags=flags)
         for name, data in resources.items():
             assert_parity(data, False, f"flags={flags} {name}", flags=flags)
         assert_parity(multi, False, f"flags={flags} multi-block", flags=flags)

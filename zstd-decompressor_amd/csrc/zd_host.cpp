@@ -184,12 +184,15 @@ struct RouteIn {
   uint32_t flags;                // ZD_F_*
 };
 struct Route {
-  bool fused = false, k4f = false, k1_seq_waves = false, fork = false, k1_fork = false;
+  bool fused = false, k4f = false, k1_seq_waves = false, fork = false, k1_fork = false, k3_lat = false;
 };
 constexpr uint32_t K4F_MIN_PER_CU = 1, K4F_MAX_PER_CU = 3;
 constexpr uint32_t FUSE_MIN_PER_CU = 1, FUSE_MAX_PER_CU = 4;
 constexpr uint32_t K1W_MAX_PER_CU = 64;
 constexpr uint32_t K3_CHAINS_PER_CU = 64;
+// K3L (one chain per wave, latency-first) while its waves fit two a SIMD:
+// beyond that K3Q's 16 chains a wave win on issue
+constexpr uint32_t K3L_MAX_PER_CU = 8;
 constexpr double FORK_MAX_FILL = 0.65;
 Route route_plan(const RouteIn& in) {
   Route r;
@@ -201,15 +204,16 @@ Route route_plan(const RouteIn& in) {
   const uint64_t slots = K3_CHAINS_PER_CU * cus, rem = in.n_seq % slots;
   r.fork = in.n_seq >= cus && rem != 0 && (double)rem <= FORK_MAX_FILL * (double)slots;
   r.k1_fork = !r.fork && in.n_huf && in.n_seq;
+  r.k3_lat = in.n_seq <= K3L_MAX_PER_CU * cus && !(in.flags & (ZD_F_SEQ_ONE_LANE | ZD_F_SEQ_NO_LATENCY));
   return r;
 }
 // The environment overrides (experiments only), read once
 struct RouteEnv {
-  int fuse = -1, k4f = -1, fork = -1, k1fork = -1;
+  int fuse = -1, k4f = -1, fork = -1, k1fork = -1, k3l = -1;
   int64_t k1w_max = -1;
   RouteEnv() {
     auto get = [](const char* n) { const char* e = getenv(n); return e ? atoi(e) : -1; };
-    fuse = get("ZD_FUSE"); k4f = get("ZD_K4F"); fork = get("ZD_FORK"); k1fork = get("ZD_K1FORK");
+    fuse = get("ZD_FUSE"); k4f = get("ZD_K4F"); fork = get("ZD_FORK"); k1fork = get("ZD_K1FORK"); k3l = get("ZD_K3L");
     if (const char* e = getenv("ZD_K1W_MAX")) k1w_max = atoll(e);
   }
 };
@@ -1651,6 +1655,7 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
     a.k1_fork = true;
   }
   a.k1_seq_waves = E.k1w_max >= 0 ? P->n_tables <= (uint64_t)E.k1w_max && !(P->flags & ZD_F_K1_LANES) : r.k1_seq_waves;
+  a.k3_lat = E.k3l >= 0 ? E.k3l == 1 && !(P->flags & (ZD_F_SEQ_ONE_LANE | ZD_F_SEQ_NO_LATENCY)) : r.k3_lat;
   P->last_fused = P->fused && !P->profile;
   if (P->last_fused) {
     a.fused = true;

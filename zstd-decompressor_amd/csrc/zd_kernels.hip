@@ -2061,6 +2061,212 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
                                  al[1], al[2], C.nseq, recs + C.seq_out);
   if (st) k3_fail(C, ci, cstate, fstate, st);
 }
+// ---------------------------------------------------------------------------
+// K3L: the latency-first FSE chain, for plans of few blocks (C3, the single
+// 100 MB frame), where a K3Q wave's 16 chains all run alone on their SIMD and
+// a step costs what one wave issues for it (~54 instructions at 4 cycles).
+// One block per wave, every lane running the same chain (wave-uniform): the
+// bit position lives in an SGPR, the bitstream window is spread over the
+// wave's lanes (lane L holds dword D + L of the stream; the 64 bits under the
+// position come by two v_readlane, no select tree and no per-step load), and
+// each LDS table entry is 64 bits: lo = nb | (extra + nb) << 8 | bad << 16
+// (nb in the low 5 bits, so it is the bfe width as it stands, and the sum of
+// the OF and ML entries is the LL state bits' offset), hi = the LDS address
+// of the next state's baseline (table + 8 x baseline), so a new state is one
+// shift-add.  The three lookups go out together, one wait.  Records are K3Q's
+// pairs, bit for bit (zd_common.h rec_pack): the states come back from the
+// addresses (LL at byte 0, ML at 4096, OF at 8192 of a 4 KiB-aligned table
+// block: state = address >> 3 & 511).  Rejects as seq_chainq: a code above
+// the maximum anywhere, the position going negative, the last step's extra
+// bits running out -- the block then goes to the exact chain.
+// ---------------------------------------------------------------------------
+constexpr uint32_t K3L_ML = 4096, K3L_OF = 8192, K3L_BYTES = 10240;   // LL at 0
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ inline uint64_t k3l_entry(uint32_t e, int k, int al, uint32_t tab) {
+  const uint32_t c = e & 63, ns = (e >> 6) & 1023;
+  uint32_t base, eb;
+  bool bad;
+  if (k == 0) { ll_code(c, &base, &eb); bad = c > 35; }
+  else if (k == 2) { ml_code(c, &base, &eb); bad = c > 52; }
+  else { eb = c; bad = c > 31; }
+  bad = bad || ns == 0 || hb32(ns) > al;
+  const uint32_t nb = bad ? 0u : (uint32_t)(al - hb32(ns));
+  const uint32_t bl = bad ? 0u : (ns << nb) - (1u << al);
+  const uint32_t lo = bad ? (1u << 16) : (nb | ((eb + nb) << 8));     // a bad entry moves nothing
+  return (uint64_t)lo | ((uint64_t)(tab + 8 * bl) << 32);
+}
+// The block's three tables (fses slots, k = 0 LL, 1 OF, 2 ML) as K3L entries
+// at LDS byte address tb (4 KiB-aligned), all 64 lanes.
+__device__ inline void k3l_tables(const uint16_t* __restrict__ fses, const CompBlock& C, const CompBlock* __restrict__ comp,
+                                  const CompState* __restrict__ cstate, uint32_t tb, int al[3], int lane) {
+  for (int k = 0; k < 3; k++) {
+    const uint32_t s = (uint32_t)C.tab_src[k];
+    al[k] = cstate[s].al[k];
+    const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+    const uint32_t t = tb + (k == 0 ? 0u : k == 2 ? K3L_ML : K3L_OF);
+    const int cnt = 1 << min(al[k], k == 1 ? 8 : 9);
+    for (int e = lane; e < cnt; e += 64) *(lds_u64*)(uintptr_t)(t + 8 * e) = k3l_entry(g[e], k, al[k], t);
+  }
+}
+// PUB (zd_k_fused): after every 16 records the chain publishes to *prog the
+// 16-record lines whose stores have completed (the line eight pairs back).
+template <bool PUB = false>
+__device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, uint32_t tb, int all, int alo, int alm,
+                          uint32_t n, uint64_t* __restrict__ out, volatile lds_u32* prog = nullptr) {
+  const int lane = threadIdx.x & 63;
+  if (bs_size == 0 || (tb & 4095) || alo > 8) return 1;
+  const uint8_t lastb = bs[bs_size - 1];
+  if (lastb == 0) return 1;
+  int32_t pos = (int32_t)(8 * (bs_size - 1)) + highbit32(lastb);   // bits above bs
+  const int32_t A = all + alo + alm;
+  if (A > pos) return 1;
+  // positions and window dwords relative to the dword-aligned address at or below bs
+  const uint8_t* bsa = (const uint8_t*)((uintptr_t)bs & ~(uintptr_t)3);
+  const int32_t boff = (int32_t)(((uintptr_t)bs & 3) * 8);
+  const uint64_t below = ((uintptr_t)bsa - (base & ~(uintptr_t)3)) >> 2;   // dwords of input below bsa
+  const int32_t dmin = below > (1u << 30) ? -(1 << 30) : -(int32_t)below;
+  auto wload = [&](int32_t D) -> uint32_t {
+    const int32_t d = max(D + lane, dmin);
+    return *(const g_u32*)(bsa + 4 * (int64_t)d);
+  };
+  // the window: dwords [D, D + 64) of the stream, one per lane; Q = the
+  // position relative to dword D (the chain's one running number: the step
+  // subtracts its bit count from it, its dword is lane Q >> 5), pos = Q + qb
+  int32_t D = ((pos + boff) >> 5) - 62;
+  int32_t Q = pos + boff - 32 * D;
+  int32_t qb = 32 * D - boff;
+  // win1: the window moved down one lane (lane L holds dword D + L + 1), so
+  // both dwords under a position come by readlane at one lane index
+  auto shl1 = [](uint32_t w) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w, 0x130, 0xf, 0xf, false); };
+  uint32_t win = wload(D);
+  uint32_t win1 = shl1(win);
+  uint32_t nxt;
+  auto bits32 = [&](int32_t q) -> uint32_t {  // 32 bits from window bit q up
+    const int idx = q >> 5;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)win, idx);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)win1, idx);
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (q & 31));
+  };
+  const uint32_t v0 = bits32(Q - A) & (uint32_t)((1ull << A) - 1);
+  uint32_t aL = tb + 8 * (v0 >> (alo + alm));
+  uint32_t aO = tb + K3L_OF + 8 * __builtin_amdgcn_ubfe(v0, alm, alo);
+  uint32_t aM = tb + K3L_ML + 8 * __builtin_amdgcn_ubfe(v0, 0, alm);
+  Q -= A;
+  uint32_t bad = 0;
+  auto lshl3_add = [](uint32_t v, uint32_t b) -> uint32_t {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(r) : "v"(v), "v"(b));
+    return r;
+  };
+  auto step = [&]() {
+    const uint64_t eL = *(const lds_u64*)(uintptr_t)aL, eM = *(const lds_u64*)(uintptr_t)aM;
+    const uint64_t eO = *(const lds_u64*)(uintptr_t)aO;
+    const uint32_t lL = (uint32_t)eL, lM = (uint32_t)eM, lO = (uint32_t)eO;
+    const uint32_t lOM = lO + lM;              // (its low 5 bits: the LL state bits' offset)
+    const uint32_t ls = lOM + lL;
+    bad |= ls;
+    Q -= __builtin_amdgcn_readfirstlane((ls >> 8) & 255);
+    const uint32_t r = bits32(Q);
+    const uint32_t vO = __builtin_amdgcn_ubfe(r, 0, lO), vM = __builtin_amdgcn_ubfe(r, lO, lM);
+    const uint32_t vL = __builtin_amdgcn_ubfe(r, lOM, lL);
+    aO = lshl3_add(vO, (uint32_t)(eO >> 32));
+    aM = lshl3_add(vM, (uint32_t)(eM >> 32));
+    aL = lshl3_add(vL, (uint32_t)(eL >> 32));
+  };
+  // a record's state field: the address's index bits (tables 4 KiB-aligned)
+  auto sx = [](uint32_t a) { return __builtin_amdgcn_ubfe(a, 3, 9); };
+  // pair (record A, record B) in K3Q's words
+  auto put = [&](uint64_t* p, uint32_t pA, uint32_t lA, uint32_t mA, uint32_t oA, uint32_t pB, uint32_t lB, uint32_t mB,
+                 uint32_t oB) {
+    const u32x4g v{sx(oA) | (sx(oB) << 10) | ((pA - pB) << 20), sx(mA) | (sx(mB) << 10), sx(lA) | (sx(lB) << 10), pA};
+    *(g_u32x4g*)p = v;
+  };
+  const uint32_t n_even = (n + 1) & ~1u;       // the spare pair
+  uint32_t pP = (uint32_t)(Q + qb), pL = aL, pM = aM, pO = aO;   // record i, kept for its pair
+  uint32_t i = 0;
+  // per window: the next one loads while this one's trips run (a trip's four
+  // steps read <= 4 x 89 bits below the position: 12 dwords), and becomes
+  // the window when fewer than 13 dwords are left below the position
+  while (i + 1 < n) {
+  if ((Q >> 5) < 13) {
+    D -= 48;
+    Q += 48 * 32;
+    qb -= 48 * 32;
+    win = nxt;
+    win1 = shl1(win);
+  }
+  nxt = wload(D - 48);
+  do {
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+      step();
+      const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
+      put(out + (slot < n ? slot : n_even), pP, pL, pM, pO, (uint32_t)(Q + qb), aL, aM, aO);
+      if constexpr (PUB) {
+        // the line ending with pair slot - 14 (seven pairs back): its store
+        // is older than the newest eight vector-memory ops (the seven pair
+        // stores since, and at most one window load)
+        if (((slot + 2) & 15) == 0 && slot + 2 >= 32) {
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if (lane == 0) *prog = (slot + 2 - 16) >> 4;
+        }
+      }
+      step();
+      pP = (uint32_t)(Q + qb); pL = aL; pM = aM; pO = aO;
+    }
+    i += 4;
+  } while (i + 1 < n && (Q >> 5) >= 13);
+  }
+  // the record the last trip kept (record i): the block's last when n - 1 == i
+  put(out + (i < n ? i : n_even), pP, pL, pM, pO, pP, pL, pM, pO);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint64_t rl = k3_reread(out, n - 1);
+  const int32_t pl = (int32_t)(uint32_t)rl;
+  const uint32_t st = (uint32_t)(rl >> 32);
+  const uint32_t lL = *(const lds_u32*)(uintptr_t)(tb + 8 * (st & 1023));
+  const uint32_t lM = *(const lds_u32*)(uintptr_t)(tb + K3L_ML + 8 * ((st >> 10) & 1023));
+  const uint32_t lO = *(const lds_u32*)(uintptr_t)(tb + K3L_OF + 8 * ((st >> 20) & 255));
+  const uint32_t ls = lL + lM + lO;
+  // the last sequence's extra bits: its count sum less its state bits
+  const int32_t E = (int32_t)(((ls >> 8) & 255) - ((lL & 31) + (lM & 31) + (lO & 31)));
+  return ((bad | ls) >> 16 || pl < 0 || E > pl) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void zd_k_sequences_l(const uint8_t* __restrict__ src,
+                                                       const CompBlock* __restrict__ comp, CompState* cstate,
+                                                       FrameState* fstate, const uint32_t* __restrict__ list,
+                                                       uint32_t n_list, const uint16_t* __restrict__ fses,
+                                                       uint64_t* __restrict__ recs, const uint8_t* __restrict__ redo) {
+  __shared__ __attribute__((aligned(4096))) uint64_t tabs[K3L_BYTES / 8];
+  const int lane = threadIdx.x;
+  const uint32_t li = blockIdx.x;
+  if (li >= n_list) return;
+  const uint32_t ci = list[li];
+  const CompBlock C = comp[ci];
+  if (redo && !redo[C.frame]) return;          // the redo pass after zd_k_fused: flagged frames only
+  const uint64_t key0 = fstate[C.frame].key;
+  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
+  const uint32_t tb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t*)tabs;
+  int al[3];
+  k3l_tables(fses, C, comp, cstate, tb, al, lane);
+  __syncthreads();
+  const CompState cs = cstate[ci];
+  const uint8_t* blk = src + C.src;
+  int st = 0;
+  if (seq_chainl(blk + cs.bs_off, cs.bs_size, (uintptr_t)src, tb, al[0], al[1], al[2], C.nseq, recs + C.seq_out) &&
+      lane == 0) {
+    const uint16_t* g[3];
+    for (int k = 0; k < 3; k++) {
+      const uint32_t s = (uint32_t)C.tab_src[k];
+      g[k] = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
+    }
+    st = K3_CHAIN<g_u16*, true>(blk + cs.bs_off, cs.bs_size, (uintptr_t)src, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1],
+                                al[0], al[1], al[2], C.nseq, recs + C.seq_out);
+  }
+  if (st) k3_fail(C, ci, cstate, fstate, st);
+}
+
 // A K3 record pair read as 8-byte halves, record i's slot on lane i (a batch
 // starting at an even record): the halves are exchanged with the partner lane
 // and the lane's record unpacked (zd_common.h).  All 64 lanes active.
@@ -3249,11 +3455,15 @@ __global__ __launch_bounds__(64) void zd_k_tables_seqw(const uint8_t* __restrict
 // so the chain wave has a SIMD to itself; publishing every 32 records)
 constexpr int FZ_FRAMES = 4;
 constexpr int FZ_WAVES = 1 + FZ_FRAMES;
-__global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
+// LAT: the chains as K3L, one wave per frame (waves 0 .. FZ_FRAMES - 1; the
+// K4 waves after them), the tables converted from the K3 format in LDS
+template <bool LAT>
+__global__ __launch_bounds__(64 * (LAT ? 2 * FZ_FRAMES : FZ_WAVES)) void zd_k_fused(
     const uint8_t* __restrict__ src, uint8_t* outbase, const FrameDesc* __restrict__ frames, FrameState* fstate,
     const BlockRec* __restrict__ blocks, const CompBlock* __restrict__ comp, CompState* cstate,
     const uint8_t* __restrict__ lits, uint64_t* __restrict__ seqs, uint16_t* __restrict__ fses,
     uint32_t n_frames, const uint32_t* k2done, uint32_t k2need, uint8_t* redo) {
+  __shared__ __attribute__((aligned(4096))) uint64_t ltabs[LAT ? FZ_FRAMES : 1][LAT ? 12288 / 8 : 1];
   __shared__ __attribute__((aligned(16))) uint16_t tabs[FZ_FRAMES * K3_TAB];
   __shared__ __attribute__((aligned(16))) uint8_t win[FZ_FRAMES][K4_WPAD + K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[FZ_FRAMES][64];
@@ -3266,10 +3476,11 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (threadIdx.x < FZ_FRAMES) prog[threadIdx.x] = trdy[threadIdx.x] = 0;
   __syncthreads();
-  if (wave > 0) {
+  constexpr int NCH = LAT ? FZ_FRAMES : 1;      // chain waves
+  if (wave >= NCH) {
     // (readfirstlane: the compiler sees the frame as wave-uniform, so the
     // table walk below runs on the scalar unit)
-    const int q = __builtin_amdgcn_readfirstlane(wave - 1);
+    const int q = __builtin_amdgcn_readfirstlane(wave - NCH);
     const uint32_t f = blockIdx.x * FZ_FRAMES + q;
     if (f >= n_frames) return;
     if (lane == 0) FZT(f, 8);
@@ -3300,6 +3511,63 @@ __global__ __launch_bounds__(64 * FZ_WAVES) void zd_k_fused(
     const K4Fuse z{(const volatile l_u32*)&prog[q], (const volatile l_u32*)&trdy[q], k2done, k2need, f};
     k4_body<true>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f, f + 1, 1, nullptr, M, &z,
                   redo);
+    return;
+  }
+  if constexpr (LAT) {
+    // wave q: frame q's chain (K3L), at the SIMD's issue priority over the K4 wave beside it
+    const int q = __builtin_amdgcn_readfirstlane(wave);
+    const uint32_t f = blockIdx.x * FZ_FRAMES + q;
+    if (f >= n_frames) return;
+    if (lane == 0) FZT(f, 0);
+    const FrameDesc F = frames[f];
+    const int32_t c = F.nblocks ? blocks[F.first_block].comp : -1;
+    const uint32_t ci = c >= 0 ? (uint32_t)c : 0;
+    CompBlock C;
+    if (c >= 0) C = comp[ci];
+    const uint64_t key0 = fstate[f].key;
+    bool ready = false;
+    for (uint32_t it = 0; it < (1u << 22) && !ready; it++) {
+      ready = *(volatile uint32_t*)&trdy[q] != 0;
+      if (!ready) __builtin_amdgcn_s_sleep(ZD_FZ_SLEEP);
+    }
+    asm volatile("" ::: "memory");
+    const FzInfo I = info[q];
+    const int al[3] = {(int)(I.al & 255), (int)((I.al >> 8) & 255), (int)((I.al >> 16) & 255)};
+    const bool build = c >= 0 && C.nseq > 0 && C.host_stage > PS_SEQ_TABLES && !C.prebuilt;
+    const bool act = ready && build && I.err == 0 && C.tab_src[0] == c && C.tab_src[1] == c && C.tab_src[2] == c &&
+                     !(key0 != KEY_NONE && key_phase(key0) == PH_PARSE) && al[1] <= 8;
+    int rej = ready ? 0 : 1;
+    if (ready && build && I.err == 0 && !act && !(key0 != KEY_NONE && key_phase(key0) == PH_PARSE)) rej = 1;
+    if (act) {
+      // the K3-format entries (nextState | count << 10, K3F_BAD) -> K3L's
+      const uint32_t tb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t*)ltabs[q];
+      const lds_u16* t16 = (const lds_u16*)tabs + q * K3_TAB;
+      for (int k = 0; k < 3; k++) {
+        const int a = al[k];
+        const lds_u16* tk = t16 + (k == 0 ? 0 : k == 2 ? K3_TL : K3_TL + K3_TM);
+        const uint32_t t = tb + (k == 0 ? 0u : k == 2 ? K3L_ML : K3L_OF);
+        for (int e = lane; e < (1 << a); e += 64) {
+          const uint32_t x = tk[e], ns = x & 1023, cnt = x >> 10;
+          const bool bad = cnt == 63 || ns == 0 || hb32(ns) > a;
+          const uint32_t nb = bad ? 0u : (uint32_t)(a - hb32(ns));
+          const uint32_t lo = bad ? (1u << 16) : (nb | (cnt << 8));
+          const uint32_t hi = t + 8 * (bad ? 0u : (ns << nb) - (1u << a));
+          *(lds_u64*)(uintptr_t)(t + 8 * e) = (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+      }
+      k4_sync();
+      __builtin_amdgcn_s_setprio(3);
+      if (lane == 0) FZT(f, 5);
+      rej = seq_chainl<true>(src + C.src + I.bo, I.bsz, (uintptr_t)src, tb, al[0], al[1], al[2], C.nseq,
+                             seqs + C.seq_out, (volatile lds_u32*)&prog[q]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) FZT(f, 2);
+    if (lane == 0) {
+      if (rej) redo[f] = 1;
+      *(volatile uint32_t*)&prog[q] = rej ? K4F_PROG_ABANDON : K4F_PROG_FINAL;
+    }
     return;
   }
   // wave 0: the chains (quad q: frame blockIdx.x * FZ_FRAMES + q)
@@ -4632,7 +4900,10 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
   if (a.events) if ((e = hipEventRecord(a.events[3], s)) != hipSuccess) return e;
   auto k3 = [&](const uint32_t* list, uint32_t n, hipStream_t st, const uint8_t* redo) {
     if (n) {
-      if (a.k3_quad)
+      if (a.k3_lat && a.k3_quad)
+        hipLaunchKernelGGL(zd_k_sequences_l, dim3(n), dim3(64), 0, st, a.src, comp, cstate, fstate, list, n,
+                           (const uint16_t*)fses, seqs, redo);
+      else if (a.k3_quad)
         hipLaunchKernelGGL(zd_k_sequences_q, dim3((n + K3Q_CHAINS - 1) / K3Q_CHAINS), dim3(64), 0, st, a.src, comp,
                            cstate, fstate, list, n, (const uint16_t*)fses, seqs, redo);
       else
@@ -4672,9 +4943,14 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     uint8_t* redo = ws + W.redo;
     const uint32_t k2need = fork ? (a.n_huf + K2_BLOCKS - 1) / K2_BLOCKS : 0;
     if ((e = dom(DOM_FUSED, 0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(zd_k_fused, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * FZ_WAVES), 0, s,
-                       a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
-                       fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
+    if (a.k3_lat)
+      hipLaunchKernelGGL(zd_k_fused<true>, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(128 * FZ_FRAMES), 0, s,
+                         a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
+                         fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
+    else
+      hipLaunchKernelGGL(zd_k_fused<false>, dim3((a.n_frames + FZ_FRAMES - 1) / FZ_FRAMES), dim3(64 * FZ_WAVES), 0, s,
+                         a.src, a.out, frames, fstate, blocks, comp, cstate, (const uint8_t*)(ws + W.lits), seqs,
+                         fses, a.n_frames, (const uint32_t*)(ws + W.k2done), k2need, redo);
     if ((e = dom(DOM_FUSED, 1)) != hipSuccess) return e;
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;

@@ -23,6 +23,7 @@ struct LaunchArgs {
   uint32_t n_k0only = 0;                   // frames K0 copies whole (FrameDesc::lds 3)
   uint32_t j_rounds = 0;                   // K4J pointer-jumping rounds launched
   uint64_t j_pieces = 0;                   // 16-byte pieces over the K4J frames' regions
+  bool k3_lat = false;     // K3 as one block per wave (zd_k_sequences_l), few-block plans
   bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block
   uint32_t j_hops = 6;                     // K4J: hops per pending word and round (ZD_J_HOPS)
   uint32_t cus = 256;                      // compute units of the device (K4J rounds' grid)

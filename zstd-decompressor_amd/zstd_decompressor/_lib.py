@@ -191,4 +191,5 @@ F_SEQ_ONE_LANE = 8     # K3 one lane per block instead of four (K3Q)
 F_NO_FUSE = 32         # K3 then K4 as two launches in few-frame plans (no zd_k_fused)
 F_K1_LANES = 64        # K1's sequence half on serial lanes in plans of <= 16,384 tables
 F_J_ONE_ROUND = 128    # test switch: K4J pointer jumping cut to one round of one hop
+F_SEQ_NO_LATENCY = 256 # K3Q instead of the one-block-per-wave K3L in plans of few blocks
 EXEC_FUSED, EXEC_K4F, EXEC_K4J = 1, 2, 4   # zd_plan_info.executors bits (include/zd.h ZD_EXEC_*)
