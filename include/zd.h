@@ -67,7 +67,7 @@ extern "C" {
 #define ZD_E_WINDOW_SIZE_TOO_BIG           (-66)
 /* Beyond the reference */
 #define ZD_E_REF_PANIC       (-90) /* the reference would panic / not terminate here */
-#define ZD_E_OUT_OF_DOMAIN   (-91) /* input outside the GPU path's parity domain (DESIGN.md §Parity domain) */
+#define ZD_E_OUT_OF_DOMAIN   (-91) /* input outside the GPU path's parity domain */
 #define ZD_E_DST_TOO_SMALL   (-92)
 #define ZD_E_INVALID_ARG     (-93)
 #define ZD_E_HIP             (-94) /* a HIP runtime call failed */
@@ -168,7 +168,7 @@ typedef struct zd_plan zd_plan;
  * it again on the streaming executor (tests/test_large_frames.py). */
 #define ZD_F_J_ONE_ROUND 128u
 
-/* zd_plan_info.executors (DESIGN.md §3): */
+/* zd_plan_info.executors (DESIGN.md §5): */
 #define ZD_EXEC_FUSED 1u   /* zd_k_fused: tables, FSE chains and execution per group of four
                               single-block frames (not while kernel profiling is on) */
 #define ZD_EXEC_K4F   2u   /* some frames execute resident in LDS (zd_k_execute_lds) */

@@ -1,4 +1,4 @@
-// Microbenchmark for a scalar-unit FSE chain (DESIGN §7, the few-frame
+// Microbenchmark for a scalar-unit FSE chain (DESIGN §8, the few-frame
 // regime): what one wave's dependent step costs when its state lives in
 // SGPRs.  One workgroup of one wave (and 1/2/4/8 waves per CU for the shared
 // scalar unit), s_memtime around each loop:
@@ -110,6 +110,43 @@ __global__ void k_movrels_chase(uint64_t* out, const uint32_t* T, uint32_t start
   if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = idx; }
 }
 
+// domain crossings: VALU -> SGPR (v_readfirstlane) -> SALU -> VALU (v_add with the SGPR), dependent
+__global__ void k_cross_vsv(uint64_t* out, uint32_t seed) {
+  uint32_t v = seed + threadIdx.x * 0, s = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(".rept 256\n\tv_readfirstlane_b32 %1, %0\n\ts_add_u32 %1, %1, 1\n\tv_add_u32 %0, %1, %0\n\t.endr"
+               : "+v"(v), "+s"(s));
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = v + s; }
+}
+// readlane chain: SGPR lane index -> v_readlane -> s_and (next index)
+__global__ void k_cross_readlane(uint64_t* out, uint32_t seed) {
+  uint32_t w = (threadIdx.x * 7 + 3) & 63, s = seed & 63;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(".rept 256\n\tv_readlane_b32 %1, %0, %1\n\ts_and_b32 %1, %1, 63\n\t.endr" : "+v"(w), "+s"(s));
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = w + s; }
+}
+// SALU -> VALU: s_add then v_add reading it, then v_readfirstlane back (the round trip of k_cross_vsv without the SALU op)
+__global__ void k_cross_vs(uint64_t* out, uint32_t seed) {
+  uint32_t v = seed, s = 0;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  asm volatile(".rept 256\n\tv_readfirstlane_b32 %1, %0\n\tv_add_u32 %0, %1, %0\n\t.endr" : "+v"(v), "+s"(s));
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = v + s; }
+}
+// ds_read_b64 chase, VGPR address straight from the loaded value (no SGPR trip)
+__global__ void k_lds_chase_v(uint64_t* out, const uint32_t* T, uint32_t start) {
+  __shared__ uint32_t L[4096];
+  for (int i = threadIdx.x; i < 4096; i += 64) L[i] = (T[i] & 4095) * 4;
+  __syncthreads();
+  uint32_t a = (start & 4095) * 4;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll 1
+  for (int i = 0; i < 256; i++) a = *(volatile __attribute__((address_space(3))) uint32_t*)(uintptr_t)a;
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = a; }
+}
 template <typename K, typename... A>
 static double run(const char* name, int per, int grid, int block, K k, uint64_t* d, A... a) {
   std::vector<uint64_t> h(2 * grid);
@@ -136,6 +173,11 @@ int main() {
     run("salu_ind4", 512, g, 64, k_salu_ind4, d, 7u);
     run("valu_dep", 512, g, 64, k_valu_dep, d, 7u);
   }
+  for (int g : {1, cus}) {
+    run("cross v->s->v (3 instr)", 256, g, 64, k_cross_vsv, d, 7u);
+    run("cross v->s->v (2 instr)", 256, g, 64, k_cross_vs, d, 7u);
+    run("readlane s->v->s (2 instr)", 256, g, 64, k_cross_readlane, d, 7u);
+  }
   std::mt19937 rng(5);
   for (uint32_t bytes : {1024u, 4096u, 8192u, 16384u, 32768u, 65536u, 1u << 20}) {
     const uint32_t n = bytes / 4;
@@ -155,6 +197,7 @@ int main() {
     }
     if (bytes >= 16384) {
       for (int g : {1, cus, 4 * cus}) run("lds_chase", 256, g, 64, k_lds_chase, d, (const uint32_t*)T, perm[0]);
+      for (int g : {1, cus, 4 * cus}) run("lds_chase_v (vgpr address)", 256, g, 64, k_lds_chase_v, d, (const uint32_t*)T, perm[0]);
     }
     if (bytes == 2048 || bytes == 4096) {
       for (int g : {1, cus, 4 * cus}) run("movrels_chase", 256, g, 64, k_movrels_chase, d, (const uint32_t*)T, perm[0]);

@@ -263,7 +263,7 @@ ZD_HD void plan_frame(const PlanCtx& X, const HostFrame& hf, const HostBlock* hb
     // K4F (whole frame resident in LDS, one 1024-thread workgroup per frame)
     // executes the frames that fit it in plans of 256-768 frames, where the
     // streaming K4 runs one round at its batch latency (C3: 0.64 vs 0.75 ms);
-    // it is slower on C4.  ZD_K4F=1 / 0 forces it on / off.
+    // it is slower on C4 (EXPERIMENTS.md).  ZD_K4F=1 / 0 forces it on / off.
     fd.lds = (X.k4f_on && X.out_len0 == 0 && cap <= K4F_CAP_BYTES) ? 1u : 0u;
   }
   if (fd.lds == 1) { if (FILL) S.list_k4f[c.k4f] = fi; c.k4f++; }
