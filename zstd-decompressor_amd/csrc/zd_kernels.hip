@@ -2185,6 +2185,9 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   const uint32_t n_even = (n + 1) & ~1u;       // the spare pair
   uint32_t pP = (uint32_t)(Q + qb), pL = aL, pM = aM, pO = aO;   // record i, kept for its pair
   uint32_t i = 0;
+  // a trip runs while i + 1 < n, so its pairs i, i + 2 are <= n, and a pair
+  // at n (n even) is the spare pair: the pair stores walk a pointer
+  uint64_t* wp = out;
   // per window: the next one loads while this one's trips run (a trip's four
   // steps read <= 4 x 89 bits below the position: 12 dwords), and becomes
   // the window when fewer than 13 dwords are left below the position
@@ -2201,21 +2204,21 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
 #pragma unroll
     for (int k = 0; k < 4; k += 2) {
       step();
-      const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
-      put(out + (slot < n ? slot : n_even), pP, pL, pM, pO, (uint32_t)(Q + qb), aL, aM, aO);
-      if constexpr (PUB) {
-        // the line ending with pair slot - 14 (seven pairs back): its store
-        // is older than the newest eight vector-memory ops (the seven pair
-        // stores since, and at most one window load)
-        if (((slot + 2) & 15) == 0 && slot + 2 >= 32) {
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-          if (lane == 0) *prog = (slot + 2 - 16) >> 4;
-        }
-      }
+      put(wp, pP, pL, pM, pO, (uint32_t)(Q + qb), aL, aM, aO);   // pair (i + k, i + k + 1)
+      wp += 2;
       step();
       pP = (uint32_t)(Q + qb); pL = aL; pM = aM; pO = aO;
     }
     i += 4;
+    if constexpr (PUB) {
+      // every 16 records: the lines up to the one that ended 16 records ago,
+      // whose stores are older than the newest eight vector-memory ops (the
+      // eight pair stores since, and at most one window load)
+      if ((i & 15) == 0 && i >= 32) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (lane == 0) *prog = (i - 16) >> 4;
+      }
+    }
   } while (i + 1 < n && (Q >> 5) >= 13);
   }
   // the record the last trip kept (record i): the block's last when n - 1 == i
