@@ -2142,8 +2142,16 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   uint32_t win = wload(D);
   uint32_t win1 = shl1(win);
   uint32_t nxt;
+  // (Q stays in a VGPR: an SGPR that the VALU writes (v_readfirstlane,
+  // v_readlane) costs ~20 cycles when the SALU reads it, ~0 when the VALU
+  // does, profiles/r6_salu_bench.txt -- so the lane index is the only
+  // crossing, and the 64-bit funnel shift is one VALU op on the SGPR pair)
   auto bits32 = [&](int32_t q) -> uint32_t {  // 32 bits from window bit q up
-    const int idx = q >> 5;
+    // (the shift stays on the VALU: left to the compiler it moved it past the
+    // v_readfirstlane onto the SALU, one crossing more on the chain)
+    int32_t qd;
+    asm("v_ashrrev_i32 %0, 5, %1" : "=v"(qd) : "v"(q));
+    const int idx = __builtin_amdgcn_readfirstlane(qd);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)win, idx);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)win1, idx);
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (q & 31));
@@ -2166,7 +2174,7 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
     const uint32_t lOM = lO + lM;              // (its low 5 bits: the LL state bits' offset)
     const uint32_t ls = lOM + lL;
     bad |= ls;
-    Q -= __builtin_amdgcn_readfirstlane((ls >> 8) & 255);
+    Q -= (ls >> 8) & 255;
     const uint32_t r = bits32(Q);
     const uint32_t vO = __builtin_amdgcn_ubfe(r, 0, lO), vM = __builtin_amdgcn_ubfe(r, lO, lM);
     const uint32_t vL = __builtin_amdgcn_ubfe(r, lOM, lL);
@@ -2192,7 +2200,7 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   // steps read <= 4 x 89 bits below the position: 12 dwords), and becomes
   // the window when fewer than 13 dwords are left below the position
   while (i + 1 < n) {
-  if ((Q >> 5) < 13) {
+  if (__builtin_amdgcn_readfirstlane(Q >> 5) < 13) {
     D -= 48;
     Q += 48 * 32;
     qb -= 48 * 32;
@@ -2219,7 +2227,7 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
         if (lane == 0) *prog = (i - 16) >> 4;
       }
     }
-  } while (i + 1 < n && (Q >> 5) >= 13);
+  } while (i + 1 < n && __builtin_amdgcn_readfirstlane(Q >> 5) >= 13);
   }
   // the record the last trip kept (record i): the block's last when n - 1 == i
   put(out + (i < n ? i : n_even), pP, pL, pM, pO, pP, pL, pM, pO);
@@ -2794,7 +2802,13 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       bool big = false;                              // batch loop left for one large sequence
       uint32_t bll = 0, bml = 0;
       uint32_t boff = 0;
-      for (;;) {
+      // One batch: the current pipeline set (records, windows, literal bytes of
+      // this batch, records of the next) in, the next set out.  The loop runs it
+      // twice a trip with the two sets' roles swapped, so no register rotation
+      // is left at the back edge (the compiler kept ~16 moves a batch there).
+      // false: the batch loop ends (an error, a large sequence, a partial batch).
+      auto batch = [&](uint64_t& recA, WinU& winA, u32x4& litA, uint64_t& recB, uint64_t& recBv_o, WinU& winB_o,
+                       u32x4& litB_o, uint64_t& recC_o) __attribute__((always_inline)) -> bool {
         const uint32_t i = s0 + lane;
         const bool valid = i < vlim;
         K4_PHASE(7);
@@ -2809,12 +2823,13 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         wait_vm();
         fl_safe = X.fl;
         // the next batch's windows and the records after it, first thing
-        const uint64_t recBv = rec_of(recB);
-        const WinU winB = win_of(recBv, s0 + 64 + lane < n);
+        recBv_o = rec_of(recB);
+        const uint64_t recBv = recBv_o;
+        winB_o = win_of(recBv, s0 + 64 + lane < n);
         if constexpr (FZ) {
-          if (!k4f_wait_recs(*fz, min(n_ld, s0 + 192))) { abandoned = true; err_key = 0; break; }
+          if (!k4f_wait_recs(*fz, min(n_ld, s0 + 192))) { abandoned = true; err_key = 0; return false; }
         }
-        const uint64_t recC = rec_at(s0 + 128 + lane);
+        recC_o = rec_at(s0 + 128 + lane);
         k4_flush(X, false);
         // Sequence values (update_symbol_value, decoders/sequence.rs:41-55):
         // K3 recorded the bit position and the three states; OF, ML, LL
@@ -2859,7 +2874,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         // the next batch's literal bytes (used only when all 64 lanes
         // execute, so from the cursor after all of them)
         const uint32_t inc_ll = wave_scan_incl(ll);
-        const u32x4 litB = lit_of(lit_cursor + (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, 63));
+        litB_o = lit_of(lit_cursor + (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, 63));
         k4_room(X);
         const uint32_t tot = ll + ml;
         const uint32_t inc_tot = wave_scan_incl(tot);
@@ -2973,7 +2988,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
           if (b < kk) {
             const int code = __builtin_amdgcn_readlane(dbad ? derr : (imp ? ZD_E_IMPOSSIBLE_VALUE : ZD_E_REF_PANIC), b);
             err_key = make_key(PH_DECODE, j, DS_EXECUTE, s0 + b, code);
-            break;
+            return false;
           }
         }
         if (k == 0) {                                  // lane 0 alone does not fit the room
@@ -2982,11 +2997,11 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
           bml = (uint32_t)__builtin_amdgcn_readlane((int)ml, 0);
           boff = (uint32_t)__builtin_amdgcn_readlane((int)off32, 0);
           rep_after(1);
-          break;
+          return false;
         }
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)inc_tot, (int)k - 1);
         const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)inc_ll, (int)k - 1);
-        if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, s0, ZD_E_OUT_OF_DOMAIN); break; }
+        if ((int64_t)X.pos + T > X.cap) { err_key = make_key(PH_LIMIT, j, LS_CAPACITY, s0, ZD_E_OUT_OF_DOMAIN); return false; }
         const bool act = (uint32_t)lane < k;
         k4_sync();                               // staged literals visible
 #if ZD_K4_OVS
@@ -3143,8 +3158,14 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         X.pos += (int32_t)T;
         s0 += k;
         K4_PHASE(5);
-        if (k < 64 || s0 >= n) break;                  // a partial batch: the pipeline restarts at s0
-        recA = recBv; winA = winB; recB = recC; litA = litB;
+        return !(k < 64 || s0 >= n);                  // a partial batch: the pipeline restarts at s0
+      };
+      uint64_t recA2 = 0, recB2 = 0;
+      WinU winA2 = winA;
+      u32x4 litA2 = litA;
+      for (;;) {
+        if (!batch(recA, winA, litA, recB, recA2, winA2, litA2, recB2)) break;
+        if (!batch(recA2, winA2, litA2, recB2, recA, winA, litA, recB)) break;
       }
       k4_flush(X, false);                            // k4_room and the large-sequence path expect it
       if (big && err_key == KEY_NONE) {
