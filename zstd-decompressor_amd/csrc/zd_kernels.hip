@@ -2162,6 +2162,10 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   uint32_t aM = tb + K3L_ML + 8 * __builtin_amdgcn_ubfe(v0, 0, alm);
   Q -= A;
   uint32_t bad = 0;
+#ifdef ZD_K3L_PROF
+  const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+  const uint64_t rp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   auto lshl3_add = [](uint32_t v, uint32_t b) -> uint32_t {
     uint32_t r;
     asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(r) : "v"(v), "v"(b));
@@ -2231,6 +2235,14 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   }
   // the record the last trip kept (record i): the block's last when n - 1 == i
   put(out + (i < n ? i : n_even), pP, pL, pM, pO, pP, pL, pM, pO);
+#ifdef ZD_K3L_PROF
+  {
+    const uint64_t tp1 = __builtin_amdgcn_s_memtime(), rp1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && blockIdx.x < 4)
+      printf("K3L block %u: %u steps, %.1f memtime ticks a step, %.1f ns a step (memrealtime 100 MHz)\n", blockIdx.x, i,
+             (double)(tp1 - tp0) / (double)max(i, 1u), 10.0 * (double)(rp1 - rp0) / (double)max(i, 1u));
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const uint64_t rl = k3_reread(out, n - 1);
   const int32_t pl = (int32_t)(uint32_t)rl;
