@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ZD_ABI_VERSION 7
+#define ZD_ABI_VERSION 8
 
 /* ------------------------------------------------------------------ */
 /* Status codes: one per reference error variant (leaf of the          */
@@ -334,6 +334,23 @@ int zd_shard_partition(const uint64_t* frame_bytes, size_t nframes, int world, s
 int zd_shard_range(const uint8_t* src, size_t n, int rank, int world, uint64_t* src_begin, uint64_t* src_end,
                    uint64_t* frame_begin, uint64_t* frame_end);
 
+/* Every rank's share at once, from one walk of the input: rank k's bytes are
+ * [src_cuts[k], src_cuts[k+1]) and its frames [frame_cuts[k],
+ * frame_cuts[k+1]) (world + 1 entries each), exactly zd_shard_range's.  Made
+ * once (on one rank, or ahead of time and kept beside the input) and handed
+ * to the ranks, so that no rank walks frames outside its own range.  Host
+ * only. */
+int zd_shard_cuts(const uint8_t* src, size_t n, int world, uint64_t* src_cuts, uint64_t* frame_cuts);
+
+/* zd_shard_range from given cuts, in time O(the rank's own range): walks only
+ * the rank's frames and checks that they tile its byte range with its frame
+ * count (the last rank's range may end in a frame that fails to index).
+ * ZD_E_INVALID_ARG when they do not, i.e. the cuts are not this input's.
+ * Host only. */
+int zd_shard_range_at(const uint8_t* src, size_t n, const uint64_t* src_cuts, const uint64_t* frame_cuts, int rank,
+                      int world, uint64_t* src_begin, uint64_t* src_end, uint64_t* frame_begin,
+                      uint64_t* frame_end);
+
 typedef struct zd_comm zd_comm;
 #define ZD_COMM_ID_BYTES 128
 
@@ -388,6 +405,14 @@ int zd_comm_gather(zd_comm* comm, const uint8_t* d_local, uint64_t local_len, in
  * the collective completed); the input's status is res->status. */
 int zd_decode_sharded(zd_comm* comm, const uint8_t* src, size_t n, uint32_t flags, uint8_t* d_root_out,
                       uint64_t root_cap, zd_gather_result* res, void* stream);
+
+/* zd_decode_sharded with the ranks' cuts given (zd_shard_cuts): each rank
+ * walks and plans only its own range.  A rank whose range does not fit the
+ * cuts still joins the collective: res->status is then ZD_E_INVALID_ARG on
+ * every rank. */
+int zd_decode_sharded_at(zd_comm* comm, const uint8_t* src, size_t n, const uint64_t* src_cuts,
+                         const uint64_t* frame_cuts, uint32_t flags, uint8_t* d_root_out, uint64_t root_cap,
+                         zd_gather_result* res, void* stream);
 
 /* ------------------------------------------------------------------ */
 /* DecodingContext mirror (decoding_context.rs:17-106): GPU-resident    */

@@ -32,7 +32,7 @@ def test_status_names():
     assert _lib.status_name(0) == "Ok"
     assert _lib.status_name(_lib.NOT_ENOUGH_BYTES) == "NotEnoughBytes"
     assert _lib.status_name(_lib.REF_PANIC) == "ReferencePanic"
-    assert _lib.lib().zd_abi_version() == 7
+    assert _lib.lib().zd_abi_version() == 8
 
 
 def test_index_resources(resources):

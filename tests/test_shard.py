@@ -218,6 +218,20 @@ def _comm_world1_worker(port, q):
                                            C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
         ok2 = st2 == 0 and res2.status == 0 and res2.total_len == len(expect) and \
             bytes(out[:len(expect)].cpu().numpy().tobytes()) == expect
+        # the same through given cuts (zd_decode_sharded_at), and cuts that
+        # are not the input's: the collective completes, res.status says so
+        sc, fc = shard.cuts(data, 1)
+        csc, cfc = (C.c_uint64 * 2)(*sc), (C.c_uint64 * 2)(*fc)
+        out.zero_()
+        res2 = _lib.GatherResult()
+        st2 = _lib.lib().zd_decode_sharded_at(comm._h, p, n, csc, cfc, 0, C.c_void_p(out.data_ptr()), out.numel(),
+                                              C.byref(res2), C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        ok2 = ok2 and st2 == 0 and res2.status == 0 and res2.total_len == len(expect) and \
+            bytes(out[:len(expect)].cpu().numpy().tobytes()) == expect
+        cfc[1] += 1
+        st2 = _lib.lib().zd_decode_sharded_at(comm._h, p, n, csc, cfc, 0, C.c_void_p(out.data_ptr()), out.numel(),
+                                              C.byref(res2), C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+        ok2 = ok2 and st2 == 0 and res2.status == _lib.INVALID_ARG and res2.total_len == 0
         # inputs that take zd_plan_decompress's re-plan, a > 12-bit Huffman
         # tree and a corrupt middle frame, each against the oracle (status,
         # first failing frame, output of the frames before it)
@@ -468,3 +482,95 @@ def test_gather_layout_multi_rank_gloo(world, fail, short):
         _, _, _, _, off, ln, *_ = got[0]
         assert out == b"".join(payloads[:upto])
         assert all(out[off[k]: off[k] + ln[k]] == payloads[k][: ln[k]] for k in range(world))
+
+
+def _cut_input():
+    from corpus import gen
+    return gen.frames(gen.text(3 << 20, seed=2), 100_000, 1)
+
+
+def test_shard_cuts_and_range_at_host():
+    """zd_shard_cuts gives every rank zd_shard_range's range from one walk;
+    zd_shard_range_at takes those cuts and walks only the rank's own frames:
+    it still gives the same range with every byte outside the range zeroed
+    (so it reads nothing there), and rejects cuts that are not the input's."""
+    import ctypes as C
+    from zstd_decompressor import _lib
+    data = _cut_input()
+    p, n, keep = _lib.buf(data)
+    for world in (1, 2, 3, 8, 41):
+        sc, fc = shard.cuts(data, world)
+        assert len(sc) == len(fc) == world + 1 and sc[0] == 0 and sc[-1] == len(data)
+        for rank in range(world):
+            v = [C.c_uint64() for _ in range(4)]
+            _lib.check(_lib.lib().zd_shard_range(p, n, rank, world, *[C.byref(x) for x in v]))
+            want = tuple(x.value for x in v)
+            assert (sc[rank], sc[rank + 1], fc[rank], fc[rank + 1]) == want
+            assert shard.range_at(data, sc, fc, rank, world) == want
+            b, e = sc[rank], sc[rank + 1]
+            blind = bytes(b) + data[b:e] + bytes(len(data) - e)
+            assert shard.range_at(blind, sc, fc, rank, world) == want
+    sc, fc = shard.cuts(data, 4)
+    for bad_sc, bad_fc in (([sc[0], sc[1] + 1] + sc[2:], fc),           # a cut inside a frame
+                           (sc, [fc[0], fc[1] + 1] + fc[2:]),           # a wrong frame count
+                           (sc[:-1] + [len(data) + 1], fc)):            # past the input
+        with pytest.raises(Exception):
+            for rank in range(4):
+                shard.range_at(data, bad_sc, bad_fc, rank, 4)
+    # a frame that fails to index: it and the rest go to the last rank, whose
+    # range_at accepts a range that ends in it
+    from zstd_decompressor.batch import frames_index
+    frames = frames_index(data)[0]
+    bad = data[: frames[20]["src_offset"]] + b"\x00\x01\x02\x03" + data[frames[20]["src_offset"]:]
+    sc, fc = shard.cuts(bad, 3)
+    assert sc[-1] == len(bad) and fc[-1] == 20
+    for rank in range(3):
+        v = [C.c_uint64() for _ in range(4)]
+        _lib.check(_lib.lib().zd_shard_range(*_lib.buf(bad)[:2], rank, 3, *[C.byref(x) for x in v]))
+        assert shard.range_at(bad, sc, fc, rank, 3) == tuple(x.value for x in v)
+
+
+def _worker_cuts(rank, world, port, q):
+    """Rank 0 walks the input once (zd_shard_cuts) and broadcasts the cuts;
+    every rank then takes its range with zd_shard_range_at, walking only its
+    own frames, and compares it with today's whole-input zd_shard_range."""
+    import ctypes as C
+    import torch.distributed as dist
+    from zstd_decompressor import _lib
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = _cut_input()
+        t = torch.zeros(2 * (world + 1), dtype=torch.int64)
+        if rank == 0:
+            sc, fc = shard.cuts(data, world)
+            t = torch.tensor(sc + fc, dtype=torch.int64)
+        dist.broadcast(t, 0)
+        sc, fc = t[: world + 1].tolist(), t[world + 1:].tolist()
+        got = shard.range_at(data, sc, fc, rank, world)
+        v = [C.c_uint64() for _ in range(4)]
+        p, n, keep = _lib.buf(data)
+        _lib.check(_lib.lib().zd_shard_range(p, n, rank, world, *[C.byref(x) for x in v]))
+        q.put((rank, got, tuple(x.value for x in v)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_at_gloo_world8():
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_cuts, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, a, b = q.get(timeout=180)
+        got[r] = (a, b)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert got[r][0] == got[r][1]
+    assert got[0][0][0] == 0 and all(got[r][0][1] == got[r + 1][0][0] for r in range(world - 1))

@@ -23,6 +23,7 @@
 
 #include "../../include/zd.h"
 #include "zd_internal.h"
+#include "zd_walk.h"
 
 namespace {
 
@@ -102,6 +103,13 @@ bool grow(uint8_t*& p, uint64_t& cap, uint64_t need) {
   return true;
 }
 
+// index_frame's block sink when only the frame walk matters
+struct CountSink {
+  size_t n = 0;
+  size_t size() const { return n; }
+  void push(const zd::HostBlock&) { n++; }
+};
+
 }  // namespace
 
 extern "C" {
@@ -127,9 +135,8 @@ int zd_shard_partition(const uint64_t* frame_bytes, size_t n, int world, size_t*
   return ZD_OK;
 }
 
-int zd_shard_range(const uint8_t* src, size_t n, int rank, int world, uint64_t* src_begin, uint64_t* src_end,
-                   uint64_t* frame_begin, uint64_t* frame_end) {
-  if (world <= 0 || rank < 0 || rank >= world || (!src && n)) return ZD_E_INVALID_ARG;
+int zd_shard_cuts(const uint8_t* src, size_t n, int world, uint64_t* src_cuts, uint64_t* frame_cuts) {
+  if (world <= 0 || (!src && n) || !src_cuts || !frame_cuts) return ZD_E_INVALID_ARG;
   // one walk of the input (zd_frames_index's): the frames before the first
   // that fails to index
   std::vector<uint64_t> off, sizes;
@@ -138,16 +145,54 @@ int zd_shard_range(const uint8_t* src, size_t n, int rank, int world, uint64_t* 
   const size_t nf = off.size();
   std::vector<size_t> cuts((size_t)world + 1);
   zd_shard_partition(sizes.data(), nf, world, cuts.data());
-  const size_t b = cuts[(size_t)rank], e = cuts[(size_t)rank + 1];
   auto off_of = [&](size_t f) -> uint64_t { return f < nf ? off[f] : (uint64_t)cons; };
-  uint64_t sb = off_of(b), se = off_of(e);
+  for (int k = 0; k <= world; k++) {
+    frame_cuts[k] = cuts[(size_t)k];
+    src_cuts[k] = off_of(cuts[(size_t)k]);
+  }
   // a frame that fails to index, and everything after it, goes to the last
   // rank: its plan stops there with that frame's status (FrameIterator)
-  if (rank == world - 1 && st != 0) se = n;
+  if (st != 0) src_cuts[world] = n;
+  return ZD_OK;
+}
+
+int zd_shard_range_at(const uint8_t* src, size_t n, const uint64_t* src_cuts, const uint64_t* frame_cuts, int rank,
+                      int world, uint64_t* src_begin, uint64_t* src_end, uint64_t* frame_begin, uint64_t* frame_end) {
+  if (world <= 0 || rank < 0 || rank >= world || (!src && n) || !src_cuts || !frame_cuts) return ZD_E_INVALID_ARG;
+  const uint64_t sb = src_cuts[rank], se = src_cuts[rank + 1];
+  const uint64_t fb = frame_cuts[rank], fe = frame_cuts[rank + 1];
+  if (sb > se || se > n || fb > fe) return ZD_E_INVALID_ARG;
+  // the rank's own frames only (FrameIterator::next from its first frame,
+  // frame.rs:94-99): they must tile [sb, se) with fe - fb frames, except that
+  // the last rank's range may end in a frame that fails to index (its plan
+  // reports it); a range that is not such a tiling is not this input's cuts
+  zd::Bytes in{src + sb, (size_t)(n - sb)};
+  uint64_t count = 0;
+  bool failed = false;
+  while ((uint64_t)(in.p - src) < se) {
+    zd::HostFrame hf;
+    CountSink S;
+    if (zd::index_frame(src, in, &hf, S)) { failed = true; break; }
+    count++;
+  }
+  const bool tiles = failed ? (rank == world - 1 && se == n) : (uint64_t)(in.p - src) == se;
+  if (!tiles || count != fe - fb) return ZD_E_INVALID_ARG;
   if (src_begin) *src_begin = sb;
   if (src_end) *src_end = se;
-  if (frame_begin) *frame_begin = b;
-  if (frame_end) *frame_end = e;
+  if (frame_begin) *frame_begin = fb;
+  if (frame_end) *frame_end = fe;
+  return ZD_OK;
+}
+
+int zd_shard_range(const uint8_t* src, size_t n, int rank, int world, uint64_t* src_begin, uint64_t* src_end,
+                   uint64_t* frame_begin, uint64_t* frame_end) {
+  if (world <= 0 || rank < 0 || rank >= world || (!src && n)) return ZD_E_INVALID_ARG;
+  std::vector<uint64_t> sc((size_t)world + 1), fc((size_t)world + 1);
+  if (int r = zd_shard_cuts(src, n, world, sc.data(), fc.data())) return r;
+  if (src_begin) *src_begin = sc[rank];
+  if (src_end) *src_end = sc[rank + 1];
+  if (frame_begin) *frame_begin = fc[rank];
+  if (frame_end) *frame_end = fc[rank + 1];
   return ZD_OK;
 }
 
@@ -250,20 +295,18 @@ int zd_comm_gather(zd_comm* c, const uint8_t* d_local, uint64_t local_len, int32
   return ZD_OK;
 }
 
-int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, uint8_t* d_root_out, uint64_t root_cap,
-                      zd_gather_result* res, void* stream) {
-  if (!c || !res || (!src && n)) return ZD_E_INVALID_ARG;
+// zd_decode_sharded(_at) once the rank's range is known
+static int decode_range(zd_comm* c, const uint8_t* src, uint64_t sb, uint64_t se, uint64_t fb, int32_t pre,
+                        uint32_t flags, uint8_t* d_root_out, uint64_t root_cap, zd_gather_result* res, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  uint64_t sb = 0, se = 0, fb = 0, fe = 0;
-  if (int r = zd_shard_range(src, n, c->rank, c->world, &sb, &se, &fb, &fe)) return r;
-  int32_t status = ZD_OK;
-  int64_t first = -1;
+  int32_t status = pre;
+  int64_t first = pre ? 0 : -1;
   uint64_t len = 0;
   uint8_t* d_out = nullptr;
   zd_plan* P = nullptr;
   // a local failure still takes part in the collective (as this rank's
   // status), so no rank is left waiting in it
-  if (se > sb) {
+  if (!pre && se > sb) {
     int err = 0;
     do {
       if ((err = zd_plan_create(src + sb, se - sb, flags, &P))) break;
@@ -294,6 +337,24 @@ int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, 
   const int g = zd_comm_gather(c, d_out, len, status, status ? (int64_t)fb + first : -1, d_root_out, root_cap, res, s);
   if (g == ZD_OK && hipStreamSynchronize(s) != hipSuccess) return fin(ZD_E_HIP);
   return fin(g);
+}
+
+int zd_decode_sharded(zd_comm* c, const uint8_t* src, size_t n, uint32_t flags, uint8_t* d_root_out, uint64_t root_cap,
+                      zd_gather_result* res, void* stream) {
+  if (!c || !res || (!src && n)) return ZD_E_INVALID_ARG;
+  uint64_t sb = 0, se = 0, fb = 0, fe = 0;
+  if (int r = zd_shard_range(src, n, c->rank, c->world, &sb, &se, &fb, &fe)) return r;
+  return decode_range(c, src, sb, se, fb, ZD_OK, flags, d_root_out, root_cap, res, stream);
+}
+
+int zd_decode_sharded_at(zd_comm* c, const uint8_t* src, size_t n, const uint64_t* src_cuts, const uint64_t* frame_cuts,
+                         uint32_t flags, uint8_t* d_root_out, uint64_t root_cap, zd_gather_result* res, void* stream) {
+  if (!c || !res || (!src && n)) return ZD_E_INVALID_ARG;
+  uint64_t sb = 0, se = 0, fb = 0, fe = 0;
+  // cuts that do not fit this rank's range fail here but still join the
+  // collective, so every rank sees ZD_E_INVALID_ARG in res->status
+  const int pre = zd_shard_range_at(src, n, src_cuts, frame_cuts, c->rank, c->world, &sb, &se, &fb, &fe);
+  return decode_range(c, src, sb, se, fb, pre, flags, d_root_out, root_cap, res, stream);
 }
 
 }  // extern "C"

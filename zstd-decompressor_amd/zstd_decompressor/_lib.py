@@ -98,6 +98,12 @@ SIGNATURES = {
     "zd_comm_gather": (C.c_int, [_vp, _vp, C.c_uint64, C.c_int32, C.c_int64, _vp, C.c_uint64,
                                  C.POINTER(GatherResult), _vp]),
     "zd_decode_sharded": (C.c_int, [_vp, _vp, _sz, C.c_uint32, _vp, C.c_uint64, C.POINTER(GatherResult), _vp]),
+    "zd_decode_sharded_at": (C.c_int, [_vp, _vp, _sz, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32, _vp,
+                                       C.c_uint64, C.POINTER(GatherResult), _vp]),
+    "zd_shard_cuts": (C.c_int, [_vp, _sz, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "zd_shard_range_at": (C.c_int, [_vp, _sz, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_int, C.c_int,
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

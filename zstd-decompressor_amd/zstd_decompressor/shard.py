@@ -52,6 +52,34 @@ def partition_native(sizes: Sequence[int], world: int) -> List[Tuple[int, int]]:
     return [(cuts[k], cuts[k + 1]) for k in range(world)]
 
 
+def cuts(data: bytes, world: int) -> Tuple[List[int], List[int]]:
+    """(src_cuts, frame_cuts), world + 1 entries each: every rank's byte and
+    frame range from one walk of the input (zd_shard_cuts).  Made on one rank
+    and broadcast, so the others walk only their own frames (range_at)."""
+    import ctypes as C
+    from . import _lib
+    p, n, keep = _lib.buf(data)
+    sc, fc = (C.c_uint64 * (world + 1))(), (C.c_uint64 * (world + 1))()
+    _lib.check(_lib.lib().zd_shard_cuts(p, n, world, sc, fc), "zd_shard_cuts")
+    return list(sc), list(fc)
+
+
+def range_at(data: bytes, src_cuts: Sequence[int], frame_cuts: Sequence[int], rank: int,
+             world: int) -> Tuple[int, int, int, int]:
+    """shard_of's (src_begin, src_end, frame_begin, frame_end) from given cuts,
+    walking only this rank's frames (zd_shard_range_at); raises if the cuts
+    are not this input's."""
+    import ctypes as C
+    from . import _lib
+    p, n, keep = _lib.buf(data)
+    sc = (C.c_uint64 * (world + 1))(*src_cuts)
+    fc = (C.c_uint64 * (world + 1))(*frame_cuts)
+    v = [C.c_uint64() for _ in range(4)]
+    _lib.check(_lib.lib().zd_shard_range_at(p, n, sc, fc, rank, world, *[C.byref(x) for x in v]),
+               "zd_shard_range_at")
+    return tuple(x.value for x in v)
+
+
 class Comm:
     """zd_comm: libzd's own RCCL communicator (one GPU per rank).  The id is
     made on rank 0 and broadcast over an initialised torch.distributed group."""
