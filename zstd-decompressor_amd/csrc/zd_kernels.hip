@@ -1354,7 +1354,10 @@ __global__ __launch_bounds__(K2_LANES) void zd_k_huffman(const uint8_t* __restri
                                                          uint32_t n_list, const uint16_t* __restrict__ luts,
                                                          uint8_t* lits, uint32_t* k2done,
                                                          const uint8_t* __restrict__ deep_pool) {
-  __shared__ __attribute__((aligned(16))) uint32_t dl[K2_BLOCKS][PR_ENTRIES];
+#ifndef ZD_K2_LDS_PAD
+#define ZD_K2_LDS_PAD 0
+#endif
+  __shared__ __attribute__((aligned(16))) uint32_t dl[K2_BLOCKS][PR_ENTRIES + ZD_K2_LDS_PAD];
   __shared__ uint32_t counts[K2_BLOCKS][4];
   __shared__ int errs[K2_BLOCKS][4];
   const int lane = threadIdx.x, b = lane >> 2, k = lane & 3;
