@@ -61,7 +61,9 @@ def _dump_ood(data, p, tag):
 def test_fuzz_structure_aware():
     """ZD_FUZZ_ITERS / ZD_FUZZ_SEED run longer campaigns (default: 600 inputs).
     A quarter of the inputs build their tables on K1's lanes (ZD_F_K1_LANES),
-    the rest on the wave-per-block build of small plans."""
+    the rest on the wave-per-block build of small plans; a third decode their
+    sequences on K3Q (ZD_F_SEQ_NO_LATENCY), the rest on K3L, small plans'
+    default chain."""
     from zstd_decompressor import _lib
     from zstd_decompressor.batch import decompress_status
     iters = int(os.environ.get("ZD_FUZZ_ITERS", "600"))
@@ -72,6 +74,7 @@ def test_fuzz_structure_aware():
         data = _mutate(r, seeds)
         p = r.random() < 0.3
         flags = _lib.F_K1_LANES if r.random() < 0.25 else 0
+        flags |= _lib.F_SEQ_NO_LATENCY if r.random() < 0.33 else 0
         ost, oout = oracle.decompress_status(data, p)
         gst, gout = decompress_status(data, p, flags)
         if gst == OUT_OF_DOMAIN:
