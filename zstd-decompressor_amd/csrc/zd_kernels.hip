@@ -2084,6 +2084,9 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
 // bits running out -- the block then goes to the exact chain.
 // ---------------------------------------------------------------------------
 constexpr uint32_t K3L_ML = 4096, K3L_OF = 8192, K3L_BYTES = 10240;   // LL at 0
+#ifndef ZD_K3L_SHADOW
+#define ZD_K3L_SHADOW 1                 // pair formatting behind the next step's table reads
+#endif
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ inline uint64_t k3l_entry(uint32_t e, int k, int al, uint32_t tab) {
@@ -2174,9 +2177,13 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
     asm("v_lshl_add_u32 %0, %1, 3, %2" : "=v"(r) : "v"(v), "v"(b));
     return r;
   };
-  auto step = [&]() {
-    const uint64_t eL = *(const lds_u64*)(uintptr_t)aL, eM = *(const lds_u64*)(uintptr_t)aM;
-    const uint64_t eO = *(const lds_u64*)(uintptr_t)aO;
+  uint64_t eL, eM, eO;
+  auto issue = [&]() {                         // the step's three table reads
+    eL = *(const lds_u64*)(uintptr_t)aL;
+    eM = *(const lds_u64*)(uintptr_t)aM;
+    eO = *(const lds_u64*)(uintptr_t)aO;
+  };
+  auto finish = [&]() {
     const uint32_t lL = (uint32_t)eL, lM = (uint32_t)eM, lO = (uint32_t)eO;
     const uint32_t lOM = lO + lM;              // (its low 5 bits: the LL state bits' offset)
     const uint32_t ls = lOM + lL;
@@ -2189,13 +2196,23 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
     aM = lshl3_add(vM, (uint32_t)(eM >> 32));
     aL = lshl3_add(vL, (uint32_t)(eL >> 32));
   };
+  auto step = [&]() { issue(); finish(); };
   // a record's state field: the address's index bits (tables 4 KiB-aligned)
   auto sx = [](uint32_t a) { return __builtin_amdgcn_ubfe(a, 3, 9); };
   // pair (record A, record B) in K3Q's words
   auto put = [&](uint64_t* p, uint32_t pA, uint32_t lA, uint32_t mA, uint32_t oA, uint32_t pB, uint32_t lB, uint32_t mB,
                  uint32_t oB) {
+#ifdef ZD_EXP_K3L_RAWPUT
+    // timing only (with ZD_K3L_PROF): each record stored as it stands, no
+    // formatting (both into the pair's slot); the chain then rejects, and the
+    // exact chain writes the records
+    *(g_u32x4g*)p = u32x4g{oA, mA, lA, pA};
+    asm volatile("" ::: "memory");
+    *(g_u32x4g*)p = u32x4g{oB, mB, lB, pB};
+#else
     const u32x4g v{sx(oA) | (sx(oB) << 10) | ((pA - pB) << 20), sx(mA) | (sx(mB) << 10), sx(lA) | (sx(lB) << 10), pA};
     *(g_u32x4g*)p = v;
+#endif
   };
   const uint32_t n_even = (n + 1) & ~1u;       // the spare pair
   uint32_t pP = (uint32_t)(Q + qb), pL = aL, pM = aM, pO = aO;   // record i, kept for its pair
@@ -2219,9 +2236,22 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
 #pragma unroll
     for (int k = 0; k < 4; k += 2) {
       step();
+#if ZD_K3L_SHADOW
+      // the pair (i + k, i + k + 1) is formatted and stored while the next
+      // step's table reads are in flight: the asm keeps its operands (and so
+      // the formatting) behind those reads, where the compiler otherwise put
+      // up to eight of its VALU ops ahead of them, on the chain's path
+      uint32_t cP = (uint32_t)(Q + qb), cL = aL, cM = aM, cO = aO;
+      issue();
+      asm volatile("" : "+v"(pP), "+v"(pL), "+v"(pM), "+v"(pO), "+v"(cP), "+v"(cL), "+v"(cM), "+v"(cO) :: "memory");
+      put(wp, pP, pL, pM, pO, cP, cL, cM, cO);
+      wp += 2;
+      finish();
+#else
       put(wp, pP, pL, pM, pO, (uint32_t)(Q + qb), aL, aM, aO);   // pair (i + k, i + k + 1)
       wp += 2;
       step();
+#endif
       pP = (uint32_t)(Q + qb); pL = aL; pM = aM; pO = aO;
     }
     i += 4;
@@ -2256,6 +2286,9 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   const uint32_t ls = lL + lM + lO;
   // the last sequence's extra bits: its count sum less its state bits
   const int32_t E = (int32_t)(((ls >> 8) & 255) - ((lL & 31) + (lM & 31) + (lO & 31)));
+#ifdef ZD_EXP_K3L_RAWPUT
+  return 1;
+#endif
   return ((bad | ls) >> 16 || pl < 0 || E > pl) ? 1 : 0;
 }
 
@@ -4491,6 +4524,12 @@ __device__ void j_fill_lits(uint32_t* st, uint64_t P0, uint32_t n, const uint8_t
   }
 }
 
+// The scatter's literal stage (ZD_JS_STAGE 0: every literal byte its own HBM
+// load and every overlapping match byte a division, the round-5 form)
+#ifndef ZD_JS_STAGE
+#define ZD_JS_STAGE 1
+#endif
+constexpr uint32_t JS_STG = 2048;
 __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ src, FrameState* fstate,
                                                     const BlockRec* __restrict__ blocks,
                                                     const CompBlock* __restrict__ comp,
@@ -4503,6 +4542,10 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
                                                     uint32_t* jst) {
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
   __shared__ uint32_t sa[65], sll[64], soff[64], slp[64];
+#if ZD_JS_STAGE
+  __shared__ __attribute__((aligned(16))) uint8_t slit_[JS_STG];
+  l_u8* const slit = (l_u8*)slit_;
+#endif
   const int lane = threadIdx.x;
   const JSegDesc SD = jsd[blockIdx.x];
   const uint32_t e = SD.jblk;
@@ -4573,11 +4616,64 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
         slp[lane] = lit_cursor + lpos;
       }
       if (lane == 0) sa[k] = T;
+#if ZD_JS_STAGE
+      // the batch's literal bytes [lit_cursor, + Lsum) staged in LDS when
+      // they fit (16 bytes a lane; the literal buffers carry 16 readable
+      // bytes past their end), else read byte by byte from HBM
+      const bool staged = lsrc && Lsum <= JS_STG;
+      if (staged)
+        for (uint32_t c = 16 * (uint32_t)lane; c < Lsum; c += 1024) *(l_u32x4*)(slit + c) = ldg16(lsrc + lit_cursor + c);
+#endif
       k4_sync();
       // the batch's bytes [pos, pos + T) in 16-byte pieces (aligned in the
       // state array): the sequence of each byte by a search of the starts
       const uint32_t g = (16 - (pos & 15)) & 15;
       const uint32_t np = T > g ? 1 + (T - g + 15) / 16 : 1;
+#if ZD_JS_STAGE
+      for (uint32_t pi = lane; pi < np; pi += 64) {
+        const uint32_t x0 = pi == 0 ? 0 : g + 16 * (pi - 1);
+        const uint32_t x1 = pi == 0 ? min(g, T) : min(T, g + 16 * pi);
+        if (x0 >= x1) continue;
+        int i = 0;
+#pragma unroll
+        for (int stp = 32; stp; stp >>= 1)
+          if (i + stp < k && sa[i + stp] <= x0) i += stp;
+        uint32_t a = sa[i], nx = sa[i + 1], l = sll[i], o = soff[i], lp = slp[i];
+        // a match byte at jj of its match copies the byte o + jj - (jj mod o)
+        // back (the reference's byte-by-byte push, decoding_context.rs:95-98):
+        // jj mod o by one division at the piece's first byte, then counted
+        uint32_t jj = 0, r = 0;
+        bool inm = x0 - a >= l;
+        if (inm) {
+          jj = x0 - a - l;
+          r = jj < o ? jj : jj % o;
+        }
+        uint32_t w[16];
+#pragma unroll
+        for (uint32_t b = 0; b < 16; b++) {
+          const uint32_t x = x0 + b;
+          w[b] = 0;
+          if (x < x1) {
+            if (b) {
+              if (x >= nx) {                   // the next sequence (one with no bytes is passed over)
+                do { i++; a = nx; nx = sa[i + 1]; } while (x >= nx);
+                l = sll[i]; o = soff[i]; lp = slp[i];
+                jj = 0; r = 0;
+                inm = l == 0;
+              } else if (inm) {
+                jj++;
+                r = r + 1 == o ? 0u : r + 1;
+              } else if (x - a >= l) {
+                inm = true;
+              }
+            }
+            const uint32_t q = lp + (x - a) - lit_cursor;   // the byte's literal, relative to the stage
+            w[b] = inm ? o + jj - r : J_FINAL | (staged ? (uint32_t)slit[q] : lsrc ? (uint32_t)lsrc[lp + (x - a)] : lfill);
+          }
+        }
+        j_store_words(st + pos + x0, w, x1 - x0);
+      }
+#else
       for (uint32_t pi = lane; pi < np; pi += 64) {
         const uint32_t x0 = pi == 0 ? 0 : g + 16 * (pi - 1);
         const uint32_t x1 = pi == 0 ? min(g, T) : min(T, g + 16 * pi);
@@ -4605,6 +4701,7 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
         }
         j_store_words(st + pos + x0, w, x1 - x0);
       }
+#endif
       k4_sync();
       lit_cursor += Lsum;
       pos += T;

@@ -89,8 +89,8 @@ class Frame:
     @staticmethod
     def parse(parser) -> "Frame":
         L = _lib.lib()
-        data = parser.remaining()
-        p, n, keep = _lib.buf(data)
+        base = parser._pos
+        p, n, keep = _lib.buf_from(parser._data, base)    # the remaining bytes, not copied
         fa = (FrameDesc * 1)()
         nf, nb, cons = C.c_size_t(), C.c_size_t(), C.c_size_t()
         # first pass: block count of the first frame
@@ -100,7 +100,7 @@ class Frame:
         ba = (BlockDesc * max(nb.value, 1))()
         L.zd_frames_index(p, n, fa, 1, C.byref(nf), ba, nb.value, C.byref(nb), C.byref(cons))
         d = fa[0]
-        raw = data[d.src_offset:d.src_offset + d.src_size]
+        raw = parser._data[base + d.src_offset:base + d.src_offset + d.src_size]
         parser.advance(d.src_offset + d.src_size)
         if d.kind == 1:
             return Frame(Skippable(d.magic, raw[8:]))
