@@ -1870,6 +1870,9 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
+#ifndef ZD_K3Q_DEFER
+#define ZD_K3Q_DEFER 0
+#endif
 template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
@@ -1920,8 +1923,20 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   }
   uint32_t mx = 0;
   int32_t ymin = 0;
+#if ZD_K3Q_DEFER
+  // ZD_K3Q_DEFER: a step's window load (for the step L on) is issued by the
+  // next step, after that step's table read, so the two VMEM issues stay off
+  // the path from the state to its table read.  pend: the position the load
+  // anchors at (the first step reloads w[L - 1] at its own anchor, a no-op)
+  int32_t pend = pos;
+  auto step = [&](WinN<N>& use, WinN<N>& prev) {
+    const uint32_t e = tab[s];
+    asm volatile("" ::: "memory");
+    prev = winn_load<N>(bs, m, pend);
+#else
   auto step = [&](WinN<N>& use) {
     const uint32_t e = tab[s];
+#endif
     mx = max(mx, e);                                // (the shadow lane's e is the LL lane's)
     const uint32_t ns = e & 1023, nb = __builtin_clz(ns) + ar;
     // the three roles' counts by three quad broadcasts and one add3 (the
@@ -1933,7 +1948,11 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     pos -= (int32_t)csum;
     ymin = min(ymin, y);
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
+#if ZD_K3Q_DEFER
+    pend = pos;
+#else
     use = winn_load<N>(bs, m, pos);
+#endif
     // the state bits sit OF | ML | LL upwards from y: offsets 0, nbO, nbO +
     // nbM (the shadow takes the LL lane's), by quad_perm [0,0,1,1] twice
     const uint32_t t = qdpp<0x50>(nb) & m0;
@@ -1947,7 +1966,11 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   for (; i + 1 < n; i += U) {
 #pragma unroll
     for (int k = 0; k < U; k += 2) {
+#if ZD_K3Q_DEFER
+      step(w[k % L], w[(k + L - 1) % L]);
+#else
       step(w[k % L]);
+#endif
       asm volatile("" ::: "memory");
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
       if constexpr (U == 4) {
@@ -1969,7 +1992,11 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
           if (role == 0) *prog = (slot + 2 - 16) >> 4;
         }
       }
+#if ZD_K3Q_DEFER
+      step(w[(k + 1) % L], w[k % L]);
+#else
       step(w[(k + 1) % L]);
+#endif
       pS = s;
       pPos = (uint32_t)pos;
     }
@@ -2084,6 +2111,9 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
 // bits running out -- the block then goes to the exact chain.
 // ---------------------------------------------------------------------------
 constexpr uint32_t K3L_ML = 4096, K3L_OF = 8192, K3L_BYTES = 10240;   // LL at 0
+#ifndef ZD_K3L_ASM
+#define ZD_K3L_ASM 1                    // the step's count sum and 64-bit funnel as one op each
+#endif
 #ifndef ZD_K3L_SHADOW
 #define ZD_K3L_SHADOW 1                 // pair formatting behind the next step's table reads
 #endif
@@ -2160,7 +2190,15 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
     const int idx = __builtin_amdgcn_readfirstlane(qd);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)win, idx);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)win1, idx);
+#if ZD_K3L_ASM
+    // one 64-bit shift of the SGPR pair (the shift count, q & 31, is off the
+    // path), where the compiler moved lo to a VGPR and used v_alignbit
+    uint64_t r;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "v"((uint32_t)q & 31u), "s"(((uint64_t)hi << 32) | lo));
+    return (uint32_t)r;
+#else
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (q & 31));
+#endif
   };
   const uint32_t v0 = bits32(Q - A) & (uint32_t)((1ull << A) - 1);
   uint32_t aL = tb + 8 * (v0 >> (alo + alm));
@@ -2186,7 +2224,12 @@ __device__ int seq_chainl(const uint8_t* bs, uint32_t bs_size, uintptr_t base, u
   auto finish = [&]() {
     const uint32_t lL = (uint32_t)eL, lM = (uint32_t)eM, lO = (uint32_t)eO;
     const uint32_t lOM = lO + lM;              // (its low 5 bits: the LL state bits' offset)
+#if ZD_K3L_ASM
+    uint32_t ls;                               // one add on the path, not two
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(ls) : "v"(lO), "v"(lM), "v"(lL));
+#else
     const uint32_t ls = lOM + lL;
+#endif
     bad |= ls;
     Q -= (ls >> 8) & 255;
     const uint32_t r = bits32(Q);
