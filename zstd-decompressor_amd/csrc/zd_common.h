@@ -475,7 +475,6 @@ struct Workspace {
   uint64_t lits, seqs, luts, fses;
   uint64_t jframes, jblkd, jblk, jseg, jsegd, jpend;    // K4J descriptors / state / round counters
   uint64_t jdone;                                       // K4J: one byte per piece, 1 once emitted
-  uint64_t jlist;                                       // K4J: u32 count + round 1's pending pieces (~0: none)
   uint64_t huge;                                        // K1: u32 count + the blocks whose trees have > 256 symbols
   uint64_t deep;                                        // K1's pool for deep trees of > 7,680 leaves: u32 used, then bytes
   uint64_t jst;                                         // K4J per-byte state words

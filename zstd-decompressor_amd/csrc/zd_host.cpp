@@ -443,7 +443,6 @@ void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint
   W.jseg = carve(sizeof(JSeg) * std::max<uint64_t>(T.jseg, 1));
   W.jpend = carve(4 * (J_MAX_ROUNDS + 1));
   W.jdone = carve(std::max<uint64_t>(j_pieces, 1));
-  W.jlist = (j_pieces && j_pieces < 0xFFFFFFFFull) ? carve(4 * (j_pieces + 1)) : ~0ull;   // piece numbers in u32
   W.jst = carve(4 * P->j_bytes + 64);
   W.redo = carve(std::max<uint64_t>(T.frames, 1));
   W.k2done = carve(4);
@@ -1603,7 +1602,6 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   if (P->n_jframes) {
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jdone, 0, std::max<uint64_t>(P->j_pieces, 1), s));
-    if (P->W.jlist != ~0ull) HIPCHK(hipMemsetAsync(P->d_ws + P->W.jlist, 0, 4, s));
   }
   LaunchArgs a{};
   a.src = d_src;

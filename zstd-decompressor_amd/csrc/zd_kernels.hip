@@ -4767,9 +4767,6 @@ __device__ inline uint32_t j_frame_of(const JFrame* __restrict__ jframes, uint32
 }
 
 typedef __attribute__((address_space(1))) uint32_t g_u32a1 __attribute__((aligned(1)));
-#ifndef ZD_J_LIST
-#define ZD_J_LIST 1                     // the sweeps walk round 1's pending list (0: every piece)
-#endif
 #ifndef ZD_JW_K
 #define ZD_JW_K 2
 #endif
@@ -4794,29 +4791,20 @@ constexpr int JW_K = ZD_JW_K;   // pieces per lane in flight (each hop issues JW
 // byte, and every chain ends at a literal the scatter wrote), so each wave
 // sweeps its own pieces until it leaves none pending, and the tail of empty
 // rounds costs one launch instead of one each.
-//
-// The pending list (jlist: a count, then piece numbers; plans of < 2^32
-// pieces): round 1 appends every piece it leaves pending, and the sweeps
-// (LIST) walk that list instead of every piece of the plan, which they used
-// to re-read for its done flag sweep after sweep (c3s: the sweeps launch
-// took 0.42 ms for the few pieces left).
-template <bool LIST>
 __global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const FrameDesc* __restrict__ frames,
                                                    FrameState* fstate, const JFrame* __restrict__ jframes,
                                                    uint32_t n_jframes, uint64_t n_pieces, uint32_t* jst,
                                                    uint32_t* pend, uint8_t* done, uint32_t hops, uint32_t r,
-                                                   uint32_t last, uint32_t sweeps, uint32_t* jlist) {
+                                                   uint32_t last, uint32_t sweeps) {
   if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
   const uint32_t x = blockIdx.x & 7, nk = gridDim.x >> 3;
   const uint32_t sub = threadIdx.x & 15, row = threadIdx.x >> 4, wrow = row & 3;
-  const uint64_t R = LIST ? (uint64_t)*(volatile uint32_t*)jlist : (n_pieces + 7) / 8;
-  const uint64_t i_first = LIST ? (uint64_t)blockIdx.x * (16 * JW_K) : (uint64_t)(blockIdx.x >> 3) * (16 * JW_K);
-  const uint64_t i_step = LIST ? (uint64_t)gridDim.x * (16 * JW_K) : (uint64_t)nk * (16 * JW_K);
+  const uint64_t R = (n_pieces + 7) / 8;
   bool mine = false;
   for (uint32_t sw = 0; sw < sweeps; sw++) {
   const bool fin = last && sw + 1 == sweeps;
   mine = false;
-  for (uint64_t i0 = i_first; i0 < R; i0 += i_step) {
+  for (uint64_t i0 = (uint64_t)(blockIdx.x >> 3) * (16 * JW_K); i0 < R; i0 += (uint64_t)nk * (16 * JW_K)) {
     uint64_t pc[JW_K], p0[JW_K], total[JW_K];
     uint32_t* st[JW_K];
     uint32_t w[JW_K], fr[JW_K];
@@ -4824,13 +4812,8 @@ __global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const Frame
 #pragma unroll
     for (int k = 0; k < JW_K; k++) {
       const uint64_t i = i0 + 16 * k + row;           // a wave's rows: four consecutive pieces per k
-      if constexpr (LIST) {
-        act[k] = i < R;
-        pc[k] = act[k] ? jlist[1 + i] : 0;
-      } else {
-        pc[k] = x * R + i;
-        act[k] = i < R && pc[k] < n_pieces;
-      }
+      pc[k] = x * R + i;
+      act[k] = i < R && pc[k] < n_pieces;
     }
     JFrame JF[JW_K];
     uint8_t dn[JW_K];
@@ -4889,17 +4872,6 @@ __global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const Frame
       if (act[k] && piece_pending) {
         mine = true;
         if (fin && sub == 0) key_min(fstate, fr[k], make_key(PH_LIMIT, 0, LS_JROUNDS, 0, ZD_E_OUT_OF_DOMAIN));
-      }
-      if (!LIST && jlist) {
-        // the wave's pending pieces onto the list: one atomic per wave
-        const uint64_t lead = __ballot(sub == 0 && act[k] && piece_pending);
-        if (lead) {
-          uint32_t base = 0;
-          if ((threadIdx.x & 63) == 0) base = atomicAdd(jlist, (uint32_t)__popcll(lead));
-          base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-          if (sub == 0 && act[k] && piece_pending)
-            jlist[1 + base + __popcll(lead & ((1ull << (threadIdx.x & 63)) - 1))] = (uint32_t)pc[k];
-        }
       }
       if (act[k] && !piece_pending) {
         // bytes of four lanes into each lane of the quad (quad_perm broadcasts)
@@ -5195,19 +5167,11 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     // round 1 one launch, the rest as one launch of sweeps
     // (one launch of all the sweeps: 1.43 ms for the rounds of c3s, against
     // 1.38 with the first round launched alone; three launches, 1.38 too)
-    // The sweeps walk round 1's pending list where the plan's piece numbers
-    // fit it (W.jlist), else every piece
     const uint32_t nr = a.j_rounds < 2 ? a.j_rounds : 2u;
-    uint32_t* jlist = (ZD_J_LIST && W.jlist != ~0ull && nr == 2) ? (uint32_t*)(ws + W.jlist) : nullptr;
-    for (uint32_t r = 1; r <= nr; r++) {
-      if (r == 2 && jlist)
-        hipLaunchKernelGGL(zd_k_jround<true>, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
-                           a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, 1u, a.j_rounds - 1, jlist);
-      else
-        hipLaunchKernelGGL(zd_k_jround<false>, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
-                           a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == nr),
-                           r == nr ? a.j_rounds - nr + 1 : 1u, jlist);
-    }
+    for (uint32_t r = 1; r <= nr; r++)
+      hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
+                         a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == nr),
+                         r == nr ? a.j_rounds - nr + 1 : 1u);
     if ((e = dom(DOM_K4J, 1)) != hipSuccess) return e;
   }
   if (a.events) if ((e = hipEventRecord(a.events[6], s)) != hipSuccess) return e;
