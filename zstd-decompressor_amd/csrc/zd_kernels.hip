@@ -4767,6 +4767,12 @@ __device__ inline uint32_t j_frame_of(const JFrame* __restrict__ jframes, uint32
 }
 
 typedef __attribute__((address_space(1))) uint32_t g_u32a1 __attribute__((aligned(1)));
+#ifndef ZD_J_SUB
+#define ZD_J_SUB 1                      // parts per region, each swept by its share of the workgroups
+#endif
+#ifndef ZD_J_XREG
+#define ZD_J_XREG 8                     // regions over the chip (8: one an XCD)
+#endif
 #ifndef ZD_JW_K
 #define ZD_JW_K 2
 #endif
@@ -4797,14 +4803,23 @@ __global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const Frame
                                                    uint32_t* pend, uint8_t* done, uint32_t hops, uint32_t r,
                                                    uint32_t last, uint32_t sweeps) {
   if (r > 1 && *(volatile uint32_t*)&pend[r - 1] == 0) return;
-  const uint32_t x = blockIdx.x & 7, nk = gridDim.x >> 3;
+  // ZD_J_XREG regions over the chip, each swept by the workgroups of 8 / XREG
+  // XCDs (workgroup b runs on XCD b mod 8)
+  constexpr uint32_t XR = ZD_J_XREG, XG = 8 / ZD_J_XREG;
+  static_assert(XR * XG == 8, "ZD_J_XREG: 1, 2, 4 or 8 regions");
+  const uint32_t x = (blockIdx.x & 7) % XR, nk = (gridDim.x >> 3) * XG;
+  const uint32_t jw = (blockIdx.x >> 3) * XG + (blockIdx.x & 7) / XR;   // the workgroup within its region
   const uint32_t sub = threadIdx.x & 15, row = threadIdx.x >> 4, wrow = row & 3;
-  const uint64_t R = (n_pieces + 7) / 8;
+  const uint64_t R = (n_pieces + XR - 1) / XR;
+  // the region in S parts, each swept by nk / S of its workgroups
+  const uint32_t S = (nk % ZD_J_SUB == 0) ? ZD_J_SUB : 1u, nu = nk / S;
+  const uint32_t rg = jw % S, u = jw / S;
+  const uint64_t Rs = (R + S - 1) / S, rb = (uint64_t)rg * Rs;
   bool mine = false;
   for (uint32_t sw = 0; sw < sweeps; sw++) {
   const bool fin = last && sw + 1 == sweeps;
   mine = false;
-  for (uint64_t i0 = (uint64_t)(blockIdx.x >> 3) * (16 * JW_K); i0 < R; i0 += (uint64_t)nk * (16 * JW_K)) {
+  for (uint64_t i0 = (uint64_t)u * (16 * JW_K); i0 < Rs; i0 += (uint64_t)nu * (16 * JW_K)) {
     uint64_t pc[JW_K], p0[JW_K], total[JW_K];
     uint32_t* st[JW_K];
     uint32_t w[JW_K], fr[JW_K];
@@ -4812,8 +4827,8 @@ __global__ __launch_bounds__(256) void zd_k_jround(uint8_t* outbase, const Frame
 #pragma unroll
     for (int k = 0; k < JW_K; k++) {
       const uint64_t i = i0 + 16 * k + row;           // a wave's rows: four consecutive pieces per k
-      pc[k] = x * R + i;
-      act[k] = i < R && pc[k] < n_pieces;
+      pc[k] = x * R + rb + i;
+      act[k] = i < Rs && rb + i < R && pc[k] < n_pieces;
     }
     JFrame JF[JW_K];
     uint8_t dn[JW_K];
