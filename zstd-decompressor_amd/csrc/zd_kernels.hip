@@ -5185,7 +5185,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     const uint32_t nr = a.j_rounds < 2 ? a.j_rounds : 2u;
     for (uint32_t r = 1; r <= nr; r++)
       hipLaunchKernelGGL(zd_k_jround, gr, dim3(256), 0, s, a.out, frames, fstate, jframes, a.n_jframes,
-                         a.j_pieces, jst, pend, ws + W.jdone, a.j_hops, r, (uint32_t)(r == nr),
+                         a.j_pieces, jst, pend, ws + W.jdone, r > 1 ? a.j_hops2 : a.j_hops, r, (uint32_t)(r == nr),
                          r == nr ? a.j_rounds - nr + 1 : 1u);
     if ((e = dom(DOM_K4J, 1)) != hipSuccess) return e;
   }
