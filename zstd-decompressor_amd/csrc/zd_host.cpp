@@ -1594,15 +1594,22 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // frame and block states are reset every launch (keys, lengths, repeat
   // offsets, flags) from device-resident copies: no host memory is read, so
   // a graph captured around this call replays the reset
+  // (one launch, zd_k_reset: frame states, block states, K1's tree list and
+  // deep pool counters, K4J's round counters and done flags; ZD_RESET_COPIES
+  // builds keep the six copy / fill launches it replaced)
+#ifndef ZD_RESET_COPIES
+  HIPCHK(launch_reset(P->d_ws, P->W, P->n_frames, P->n_comps, P->n_jframes != 0, P->j_pieces, s));
+#else
   HIPCHK(hipMemcpyAsync(P->d_ws + P->W.frame_state, P->d_ws + P->W.frame_state0,
                         P->n_frames * sizeof(FrameState), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipMemsetAsync(P->d_ws + P->W.comp_state, 0, std::max<uint64_t>(P->n_comps, 1) * sizeof(CompState), s));
-  HIPCHK(hipMemsetAsync(P->d_ws + P->W.huge, 0, 4, s));   // K1's list of trees of more than 256 symbols
-  HIPCHK(hipMemsetAsync(P->d_ws + P->W.deep, 0, 4, s));   // and its deep-tree symbol pool
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.huge, 0, 4, s));
+  HIPCHK(hipMemsetAsync(P->d_ws + P->W.deep, 0, 4, s));
   if (P->n_jframes) {
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jpend, 0, 4 * (J_MAX_ROUNDS + 1), s));
     HIPCHK(hipMemsetAsync(P->d_ws + P->W.jdone, 0, std::max<uint64_t>(P->j_pieces, 1), s));
   }
+#endif
   LaunchArgs a{};
   a.src = d_src;
   a.src_size = P->info.src_bytes;

@@ -2412,11 +2412,8 @@ __device__ inline uint64_t rec_lane(uint64_t raw, int lane) {
 #endif
 constexpr int K4_W = ZD_K4_W;                 // history kept after a slide
 constexpr int K4_B = ZD_K4_B;                 // room kept for a batch (a slide when less is left)
-#ifndef ZD_K4_GSTAB
-#define ZD_K4_GSTAB 0
-#endif
 #ifndef ZD_K4_C
-#define ZD_K4_C (ZD_K4_GSTAB ? 7072 : 7200)   // (GSTAB: 7,072 + 16 + 64 + 528 + 512 = 8 KiB, five waves per SIMD)
+#define ZD_K4_C 7200
 #endif
 constexpr int K4_C = ZD_K4_C;                 // window bytes
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -2657,7 +2654,7 @@ __device__ inline uint32_t wave_scan_incl(uint32_t x) {
 }
 
 #ifndef ZD_K4_MINW
-#define ZD_K4_MINW (ZD_K4_GSTAB ? 5 : 4)
+#define ZD_K4_MINW 4
 #endif
 #ifndef ZD_K4_CODELUT
 #define ZD_K4_CODELUT 1
@@ -2740,10 +2737,7 @@ __device__ inline bool k4f_wait_recs(const K4Fuse& z, uint32_t rec_end) {
   return false;
 }
 
-// GS: the block's LL / OF / ML symbols read from its FSE slots in HBM (u16
-// loads issued a batch ahead, beside the next batch's records) instead of
-// an LDS copy, so a wave's LDS fits five waves per SIMD (ZD_K4_GSTAB)
-template <bool FZ, bool GS = false>
+template <bool FZ>
 __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __restrict__ src, uint8_t* outbase,
                                                    const FrameDesc* __restrict__ frames, FrameState* fstate,
                                                    const BlockRec* __restrict__ blocks,
@@ -2855,21 +2849,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
     const bool direct = C.seq_direct != 0;
     // the block's LL/OF/ML symbols (K1's sym entries, zd_common.h) -> LDS
     const uint8_t* bsp = src + C.src + CS.bs_off;
-    const uint16_t* gsym[3] = {nullptr, nullptr, nullptr};
-    if (GS && n && !direct) {
-      for (int k = 0; k < 3; k++) {
-        const uint32_t s = (uint32_t)C.tab_src[k];
-        gsym[k] = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
-      }
-    }
-    // the symbols of a record's three states (the slot entries, symbol in
-    // bits 0-5; states < 512 in any table a block decodes with)
-    struct Sym3 { uint32_t l, o, m; };
-    auto sym_of = [&](uint64_t r) -> Sym3 {
-      const uint32_t stt = (uint32_t)(r >> 32);
-      return Sym3{gsym[0][stt & 511], gsym[1][(stt >> 20) & 511], gsym[2][(stt >> 10) & 511]};
-    };
-    if (!GS && n && !direct) {
+    if (n && !direct) {
       for (int k = 0; k < 3; k++) {
         const uint32_t s = (uint32_t)C.tab_src[k];
         const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
@@ -2910,8 +2890,6 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       uint64_t recB = rec_at(s0 + 64 + lane);
       WinU winA = win_of(recA, s0 + lane < vlim);
       u32x4 litA = lit_of(lit_cursor);
-      Sym3 syA{0, 0, 0};
-      if (GS && !direct) syA = sym_of(recA);
       bool big = false;                              // batch loop left for one large sequence
       uint32_t bll = 0, bml = 0;
       uint32_t boff = 0;
@@ -2921,7 +2899,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       // is left at the back edge (the compiler kept ~16 moves a batch there).
       // false: the batch loop ends (an error, a large sequence, a partial batch).
       auto batch = [&](uint64_t& recA, WinU& winA, u32x4& litA, uint64_t& recB, uint64_t& recBv_o, WinU& winB_o,
-                       u32x4& litB_o, uint64_t& recC_o, Sym3& syA, Sym3& syB_o) __attribute__((always_inline)) -> bool {
+                       u32x4& litB_o, uint64_t& recC_o) __attribute__((always_inline)) -> bool {
         const uint32_t i = s0 + lane;
         const bool valid = i < vlim;
         K4_PHASE(7);
@@ -2939,9 +2917,6 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
         recBv_o = rec_of(recB);
         const uint64_t recBv = recBv_o;
         winB_o = win_of(recBv, s0 + 64 + lane < n);
-        if constexpr (GS) {
-          if (!direct) syB_o = sym_of(recBv);
-        }
         if constexpr (FZ) {
           if (!k4f_wait_recs(*fz, min(n_ld, s0 + 192))) { abandoned = true; err_key = 0; return false; }
         }
@@ -2957,13 +2932,8 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
             seq_values(recA, C.seq_side, i, &ll, &ml, &ofv);
             giant = ofv == DIRECT_GIANT && !C.seq_side;
           } else {
-            uint32_t llc, mlc, ofc;
-            if constexpr (GS) {
-              llc = syA.l & 63; mlc = syA.m & 63; ofc = syA.o & 31;
-            } else {
-              const uint32_t stt = (uint32_t)(recA >> 32);
-              llc = stab[0][stt & 1023]; mlc = stab[2][(stt >> 10) & 1023]; ofc = stab[1][stt >> 20] & 31;
-            }
+            const uint32_t stt = (uint32_t)(recA >> 32);
+            const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
             uint32_t llbase, llb, mlbase, mlb;
 #if ZD_K4_CODELUT
             const uint32_t cl = codelut[0][llc], cm = codelut[1][mlc];
@@ -3284,10 +3254,9 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       uint64_t recA2 = 0, recB2 = 0;
       WinU winA2 = winA;
       u32x4 litA2 = litA;
-      Sym3 syA2{0, 0, 0};
       for (;;) {
-        if (!batch(recA, winA, litA, recB, recA2, winA2, litA2, recB2, syA, syA2)) break;
-        if (!batch(recA2, winA2, litA2, recB2, recA, winA, litA, recB, syA2, syA)) break;
+        if (!batch(recA, winA, litA, recB, recA2, winA2, litA2, recB2)) break;
+        if (!batch(recA2, winA2, litA2, recB2, recA, winA, litA, recB)) break;
       }
       k4_flush(X, false);                            // k4_room and the large-sequence path expect it
       if (big && err_key == KEY_NONE) {
@@ -3345,17 +3314,11 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   // (16 bytes of padding below the window: pass 0 reads up to 15 bytes before a match source)
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_WPAD + K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
-#if !ZD_K4_GSTAB
   __shared__ __attribute__((aligned(16))) uint8_t stab[3 * FSE_TAB];   // LL | OF | ML symbols of the block
-#endif
   __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
   __shared__ uint32_t codelut[2 * 64];
-#if ZD_K4_GSTAB
-  const K4Lds M{(l_u8*)win + K4_WPAD, (l_u8*)pat, nullptr, (l_u8*)stg, (l_u32*)codelut};
-#else
   const K4Lds M{(l_u8*)win + K4_WPAD, (l_u8*)pat, (l_u8*)stab, (l_u8*)stg, (l_u32*)codelut};
-#endif
-  k4_body<false, ZD_K4_GSTAB != 0>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f_begin + blockIdx.x, f_end,
+  k4_body<false>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f_begin + blockIdx.x, f_end,
                  gridDim.x, redo, M, nullptr, nullptr);
 }
 
@@ -5251,6 +5214,41 @@ extern "C" int zd_debug_k1_prof(uint64_t out[8], int reset) {
 }
 namespace zd {
 #endif
+// The per-launch state reset of zd_decode_async in one launch: frame states
+// from their device copies, block states, K1's tree list and deep-pool
+// counters, K4J's round counters and done flags (six copy / fill launches
+// before, ~5 us each on the path of a few-frame plan).
+__global__ __launch_bounds__(256) void zd_k_reset(uint8_t* ws, Workspace W, uint64_t fs_words, uint64_t cs_words,
+                                                  uint32_t jp_words, uint64_t jdone_bytes) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, nt = (uint64_t)gridDim.x * 256;
+  uint32_t* fs = (uint32_t*)(ws + W.frame_state);
+  const uint32_t* fs0 = (const uint32_t*)(ws + W.frame_state0);
+  for (uint64_t i = t; i < fs_words; i += nt) fs[i] = fs0[i];
+  uint32_t* cs = (uint32_t*)(ws + W.comp_state);
+  for (uint64_t i = t; i < cs_words; i += nt) cs[i] = 0;
+  if (t == 0) {
+    *(uint32_t*)(ws + W.huge) = 0;
+    *(uint32_t*)(ws + W.deep) = 0;
+  }
+  uint32_t* jp = (uint32_t*)(ws + W.jpend);
+  for (uint64_t i = t; i < jp_words; i += nt) jp[i] = 0;
+  u32x4* jd = (u32x4*)(ws + W.jdone);
+  const uint64_t n16 = jdone_bytes / 16;
+  for (uint64_t i = t; i < n16; i += nt) jd[i] = (u32x4){0, 0, 0, 0};
+  if (t < jdone_bytes % 16) (ws + W.jdone)[16 * n16 + t] = 0;
+}
+hipError_t launch_reset(uint8_t* ws, const Workspace& W, uint64_t n_frames, uint64_t n_comps, bool k4j,
+                        uint64_t j_pieces, hipStream_t s) {
+  const uint64_t fs_words = n_frames * sizeof(FrameState) / 4, cs_words = std::max<uint64_t>(n_comps, 1) * sizeof(CompState) / 4;
+  const uint32_t jp_words = k4j ? (uint32_t)(J_MAX_ROUNDS + 1) : 0u;
+  const uint64_t jdone = k4j ? std::max<uint64_t>(j_pieces, 1) : 0;
+  const uint64_t work = std::max(std::max(fs_words, cs_words), jdone / 16 + 16);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (work + 1023) / 1024);
+  static_assert(sizeof(FrameState) % 4 == 0 && sizeof(CompState) % 4 == 0, "zd_k_reset: u32 words");
+  hipLaunchKernelGGL(zd_k_reset, dim3(grid), dim3(256), 0, s, ws, W, fs_words, cs_words, jp_words, jdone);
+  return hipGetLastError();
+}
+
 hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* d_from, const uint64_t* d_to,
                           const uint64_t* d_len, uint32_t n, hipStream_t s) {
   if (!n) return hipSuccess;

@@ -42,6 +42,10 @@ struct LaunchArgs {
 // K1 table parse/build -> K2 Huffman literals -> K3 FSE sequences -> K4 execute.
 hipError_t launch_pipeline(const LaunchArgs& a);
 
+// zd_decode_async's state reset (frame / block states, K1 and K4J counters, K4J done flags).
+hipError_t launch_reset(uint8_t* ws, const Workspace& W, uint64_t n_frames, uint64_t n_comps, bool k4j,
+                        uint64_t j_pieces, hipStream_t s);
+
 // Copies frame outputs from staging (at cap offsets) to exact offsets.
 hipError_t launch_compact(const uint8_t* staging, uint8_t* dst, const uint64_t* d_from,
                           const uint64_t* d_to, const uint64_t* d_len, uint32_t n, hipStream_t s);
