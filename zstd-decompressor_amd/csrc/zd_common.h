@@ -479,7 +479,6 @@ struct Workspace {
   uint64_t deep;                                        // K1's pool for deep trees of > 7,680 leaves: u32 used, then bytes
   uint64_t jst;                                         // K4J per-byte state words
   uint64_t redo, k2done;                                // zd_k_fused: frames for the redo pass, K2's finished workgroups
-  uint64_t tready;                                      // zd_k_sequences_ls: u32 per block, 1 once its tables are written
   uint64_t hframes;                                     // device-built plans: the walk's frame index (zd_walk.h HostFrame)
   uint64_t total;
 };

@@ -446,7 +446,6 @@ void carve_tail(zd_plan* P, Workspace& W, const PlanCounts& T, uint64_t& o, uint
   W.jst = carve(4 * P->j_bytes + 64);
   W.redo = carve(std::max<uint64_t>(T.frames, 1));
   W.k2done = carve(4);
-  W.tready = carve(4 * std::max<uint64_t>(T.comps, 1));
 }
 // The plan's array counts from the totals
 void plan_totals(zd_plan* P, const PlanCounts& T, bool fused) {

@@ -2111,9 +2111,6 @@ __global__ __launch_bounds__(64) void zd_k_sequences_q(const uint8_t* __restrict
 // bits running out -- the block then goes to the exact chain.
 // ---------------------------------------------------------------------------
 constexpr uint32_t K3L_ML = 4096, K3L_OF = 8192, K3L_BYTES = 10240;   // LL at 0
-#ifndef ZD_K3L_SELF
-#define ZD_K3L_SELF 1                   // K3L builds its blocks' sequence tables (zd_k_sequences_ls)
-#endif
 #ifndef ZD_K3L_ASM
 #define ZD_K3L_ASM 1                    // the step's count sum and 64-bit funnel as one op each
 #endif
@@ -3567,77 +3564,6 @@ __global__ __launch_bounds__(64) void zd_k_tables_seqw(const uint8_t* __restrict
   const CompBlock C = comp[ci];
   if (C.prebuilt || C.nseq == 0 || C.host_stage <= PS_SEQ_TABLES) return;
   fz_tables(src, C, ci, cstate, fstate, fses, W, nullptr, I, (int)threadIdx.x, C.frame);
-}
-
-// K3L with its block's sequence tables built by the same wave (fz_tables:
-// the slot, CompState and parse error key as zd_k_tables_seqw writes them),
-// for plans whose K1 sequence half would otherwise be a launch of one wave a
-// block ahead of every chain (c3s: 54 us on the path); zd_k_tables_seqw
-// still runs on the aux stream over every block that needs tables (the same
-// values: the parse errors of blocks no chain runs for, and the tables of
-// blocks K4J reads), joined before the executors.  A table in Repeat mode is
-// an earlier block's (frame.rs order): that block's wave publishes tready
-// once its slot and CompState are written (agent-scope release), and this
-// wave waits for it (acquire).  Waves are dispatched in list order, so the
-// earlier block's wave is running or done; a wait past its bound is out of
-// the GPU path's domain.
-__global__ __launch_bounds__(64) void zd_k_sequences_ls(const uint8_t* __restrict__ src,
-                                                        const CompBlock* __restrict__ comp, CompState* cstate,
-                                                        FrameState* fstate, const uint32_t* __restrict__ list,
-                                                        uint32_t n_list, uint16_t* fses, uint64_t* __restrict__ recs,
-                                                        uint32_t* tready) {
-  __shared__ __attribute__((aligned(4096))) uint64_t tabs[K3L_BYTES / 8];
-  __shared__ __attribute__((aligned(16))) FzK1 W;
-  __shared__ FzInfo I;
-  const int lane = threadIdx.x;
-  const uint32_t li = blockIdx.x;
-  if (li >= n_list) return;
-  const uint32_t ci = (uint32_t)__builtin_amdgcn_readfirstlane((int)list[li]);
-  const CompBlock C = comp[ci];
-  const bool build = !C.prebuilt && C.nseq > 0 && C.host_stage > PS_SEQ_TABLES;
-  if (build) fz_tables(src, C, ci, cstate, fstate, fses, W, nullptr, I, lane, C.frame);
-  // publish this block's tables (every wave of the list does, whatever follows)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  if (lane == 0) __hip_atomic_store(&tready[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  k4_sync();
-  if (build && I.err) return;                      // Block::parse fails at this block's tables
-  const uint64_t key0 = fstate[C.frame].key;
-  if (key0 != KEY_NONE && key_phase(key0) == PH_PARSE) return;
-  // the Repeat-mode sources' tables
-  bool ok = true;
-  for (int k = 0; k < 3; k++) {
-    const uint32_t sb = (uint32_t)C.tab_src[k];
-    if (sb == ci) continue;
-    bool rdy = false;
-    for (uint32_t it = 0; it < (1u << 22) && !rdy; it++) {
-      rdy = __hip_atomic_load(&tready[sb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-      if (!rdy) __builtin_amdgcn_s_sleep(2);
-    }
-    ok = ok && rdy;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (!ok) {
-    if (lane == 0) key_min(fstate, C.frame, make_key(PH_LIMIT, C.block_in_frame, LS_CAPACITY, 0, ZD_E_OUT_OF_DOMAIN));
-    return;
-  }
-  const uint32_t tb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint64_t*)tabs;
-  int al[3];
-  k3l_tables(fses, C, comp, cstate, tb, al, lane);
-  __syncthreads();
-  const uint32_t bo = build ? I.bo : cstate[ci].bs_off, bsz = build ? I.bsz : cstate[ci].bs_size;
-  const uint8_t* blk = src + C.src;
-  int st = 0;
-  if (seq_chainl(blk + bo, bsz, (uintptr_t)src, tb, al[0], al[1], al[2], C.nseq, recs + C.seq_out) && lane == 0) {
-    const uint16_t* g[3];
-    for (int k = 0; k < 3; k++) {
-      const uint32_t sb = (uint32_t)C.tab_src[k];
-      g[k] = fses + (uint64_t)comp[sb].fse_slot * FSE_SLOT + k * FSE_TAB;
-    }
-    st = K3_CHAIN<g_u16*, true>(blk + bo, bsz, (uintptr_t)src, (g_u16*)g[0], (g_u16*)g[2], (g_u16*)g[1], al[0], al[1],
-                                al[2], C.nseq, recs + C.seq_out);
-  }
-  if (st) k3_fail(C, ci, cstate, fstate, st);
 }
 
 // (measured on C3, within noise: the chain wave at s_setprio 3; eight waves
@@ -5140,16 +5066,12 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     hipLaunchKernelGGL(zd_k_tables_seqw, dim3(a.n_tables), dim3(64), 0, st, a.src, comp, cstate, fstate,
                        (const uint32_t*)(ws + W.list_tables), a.n_tables, fses);
   };
-  // K3L building its blocks' sequence tables itself (zd_k_sequences_ls):
-  // the forked few-block plans, where the sequence half is one wave a block;
-  // it then runs on the aux stream, off the chains' path
-  const bool k3ls = ZD_K3L_SELF && fork && !fz && a.k1_seq_waves && a.k3_lat && a.k3_quad && a.n_seq;
   if (a.n_tables) {
     if (fz) {                                  // the sequence half runs in zd_k_fused
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, s2, true);
     } else if (a.k1_seq_waves) {               // few blocks: the sequence half one wave per block
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, k1f ? a.aux : s2, true);
-      k1seqw(k3ls ? s2 : s);
+      k1seqw(s);
     } else if (fork || k1f) {
       k1(zd_k_tables<false, 1>, zd_k_tables<true, 1>, k1f ? a.aux : s2, true);
       k1(zd_k_tables<false, 2>, zd_k_tables<true, 2>, s, false);
@@ -5229,11 +5151,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
     k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, redo);
     if ((e = k4(0, a.n_frames, s, redo)) != hipSuccess) return e;
   } else {
-    if (k3ls)
-      hipLaunchKernelGGL(zd_k_sequences_ls, dim3(a.n_seq), dim3(64), 0, s, a.src, comp, cstate, fstate,
-                         (const uint32_t*)(ws + W.list_seq), a.n_seq, fses, seqs, (uint32_t*)(ws + W.tready));
-    else
-      k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, nullptr);
+    k3((const uint32_t*)(ws + W.list_seq), a.n_seq, s, nullptr);
     if (fork)
       if ((e = hipStreamWaitEvent(s, a.join, 0)) != hipSuccess) return e;
     if (a.events) if ((e = hipEventRecord(a.events[4], s)) != hipSuccess) return e;
@@ -5301,15 +5219,13 @@ namespace zd {
 // counters, K4J's round counters and done flags (six copy / fill launches
 // before, ~5 us each on the path of a few-frame plan).
 __global__ __launch_bounds__(256) void zd_k_reset(uint8_t* ws, Workspace W, uint64_t fs_words, uint64_t cs_words,
-                                                  uint64_t tr_words, uint32_t jp_words, uint64_t jdone_bytes) {
+                                                  uint32_t jp_words, uint64_t jdone_bytes) {
   const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x, nt = (uint64_t)gridDim.x * 256;
   uint32_t* fs = (uint32_t*)(ws + W.frame_state);
   const uint32_t* fs0 = (const uint32_t*)(ws + W.frame_state0);
   for (uint64_t i = t; i < fs_words; i += nt) fs[i] = fs0[i];
   uint32_t* cs = (uint32_t*)(ws + W.comp_state);
   for (uint64_t i = t; i < cs_words; i += nt) cs[i] = 0;
-  uint32_t* tr = (uint32_t*)(ws + W.tready);
-  for (uint64_t i = t; i < tr_words; i += nt) tr[i] = 0;
   if (t == 0) {
     *(uint32_t*)(ws + W.huge) = 0;
     *(uint32_t*)(ws + W.deep) = 0;
@@ -5329,8 +5245,7 @@ hipError_t launch_reset(uint8_t* ws, const Workspace& W, uint64_t n_frames, uint
   const uint64_t work = std::max(std::max(fs_words, cs_words), jdone / 16 + 16);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (work + 1023) / 1024);
   static_assert(sizeof(FrameState) % 4 == 0 && sizeof(CompState) % 4 == 0, "zd_k_reset: u32 words");
-  hipLaunchKernelGGL(zd_k_reset, dim3(grid), dim3(256), 0, s, ws, W, fs_words, cs_words,
-                     std::max<uint64_t>(n_comps, 1), jp_words, jdone);
+  hipLaunchKernelGGL(zd_k_reset, dim3(grid), dim3(256), 0, s, ws, W, fs_words, cs_words, jp_words, jdone);
   return hipGetLastError();
 }
 
