@@ -36,7 +36,10 @@ step c5_L19 900 python bench.py --workload c5 --level 19 --unique-mib 256 --repl
 step c2 600 python bench.py --workload c2 &&
 step c3 600 python bench.py --workload c3 &&
 step c3s 600 python bench.py --workload c3s &&
-step c3_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_c3 -o run --output-format csv -- python bench.py --workload c3 --no-cpu-baseline --no-host-io || exit 1
+step c3_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_c3 -o run --output-format csv -- python bench.py --workload c3 --no-cpu-baseline --no-host-io &&
+step c3s_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_c3s -o run --output-format csv -- python bench.py --workload c3s --no-cpu-baseline --no-host-io &&
+step c2_1GiB 600 python bench.py --workload c2 --c2-mib 1024 --no-host-io &&
+step frame_parse 300 python scripts/time_frame_parse.py || exit 1
 fi
 if [[ $part == *c* ]]; then       # one rank's share of the strong-scaled C4 on 8 / 4 / 2 GPUs, alone on one GPU
 step share8 600 python bench.py --unique-mib 160 --replicas 8 --no-cpu-baseline --no-host-io &&
