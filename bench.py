@@ -335,6 +335,7 @@ def main():
                     help="N>1: one corpus split across the ranks (strong) or one corpus per rank (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="time the decode's launches, not a captured HIP graph of them")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use")
     ap.add_argument("--corpus-cache", default=os.environ.get("ZD_CORPUS_CACHE"),
                     help="directory to keep the generated corpus in between runs (experiments)")
@@ -453,6 +454,24 @@ def main():
     st, total, _, _, first = plan.results(d_dst.data_ptr(), sptr)
     assert args.experiment or (st == 0 and total == info.out_bytes), (st, total, first)
 
+    # The timed steps replay one decode captured in a HIP graph (zd_decode_async
+    # is graph-safe: no allocation, no host memory read, its fork stream made at
+    # plan time; tests/test_gpu_parity.py test_hip_graph_capture_replay): the
+    # same launches, without a host launch per kernel.  --no-graph times the
+    # launches themselves.
+    timed_step = step
+    if not args.no_graph:
+        cap = torch.cuda.Stream(dev)
+        graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(dev)
+        with torch.cuda.graph(graph, stream=cap):
+            plan.decode_async(d_src.data_ptr(), d_dst.data_ptr(), info.out_bytes, cap.cuda_stream)
+        torch.cuda.synchronize(dev)
+        timed_step = graph.replay
+        for _ in range(args.warmup):
+            timed_step()
+        torch.cuda.synchronize(dev)
+
     # ---- timed region ----
     if dist:
         dist.barrier()
@@ -461,7 +480,7 @@ def main():
     t_wall = time.time()
     ev0.record(stream)
     for _ in range(args.steps):
-        step()
+        timed_step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     t_wall = time.time() - t_wall
@@ -685,6 +704,8 @@ def main():
                                  "roofline.frac are not directly comparable to a real-enwik run",
                 "parallelism": (f"share {prank}/{pworld} alone" if args.share else
                                 f"frame-sharded x{world}" if strong else f"replicas x{world}"),
+                "step": "zd_decode_async over every resident frame" +
+                        (", replayed from a captured HIP graph" if not args.no_graph else ", launched per step"),
             },
             "roofline": {
                 "bound": "hbm",
