@@ -335,7 +335,7 @@ def main():
                     help="N>1: one corpus split across the ranks (strong) or one corpus per rank (weak)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-graph", action="store_true", help="time the decode's launches, not a captured HIP graph of them")
+    ap.add_argument("--graph", action="store_true", help="time a captured HIP graph of the decode, not its launches")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use")
     ap.add_argument("--corpus-cache", default=os.environ.get("ZD_CORPUS_CACHE"),
                     help="directory to keep the generated corpus in between runs (experiments)")
@@ -454,13 +454,15 @@ def main():
     st, total, _, _, first = plan.results(d_dst.data_ptr(), sptr)
     assert args.experiment or (st == 0 and total == info.out_bytes), (st, total, first)
 
-    # The timed steps replay one decode captured in a HIP graph (zd_decode_async
-    # is graph-safe: no allocation, no host memory read, its fork stream made at
-    # plan time; tests/test_gpu_parity.py test_hip_graph_capture_replay): the
-    # same launches, without a host launch per kernel.  --no-graph times the
-    # launches themselves.
+    # --graph: the timed steps replay one decode captured in a HIP graph
+    # (zd_decode_async is graph-safe: no allocation, no host memory read, its
+    # fork stream made at plan time; tests/test_gpu_parity.py
+    # test_hip_graph_capture_replay).  Not the default: in the captured graph
+    # the forked K2 ran before zd_k_fused instead of beside it (C3 2.07 ms a
+    # step against 1.42) and a short step paid the graph launch (C2 64 MiB
+    # 27 us against 19); profiles/r6_graph_replay_ab.txt.
     timed_step = step
-    if not args.no_graph:
+    if args.graph:
         cap = torch.cuda.Stream(dev)
         graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(dev)
@@ -705,7 +707,7 @@ def main():
                 "parallelism": (f"share {prank}/{pworld} alone" if args.share else
                                 f"frame-sharded x{world}" if strong else f"replicas x{world}"),
                 "step": "zd_decode_async over every resident frame" +
-                        (", replayed from a captured HIP graph" if not args.no_graph else ", launched per step"),
+                        (", replayed from a captured HIP graph" if args.graph else ", launched per step"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-6 A/B 9: the timed steps replayed from a captured HIP graph (bench.py
-# default) against launched per step (--no-graph), on c3s, C3, C2 and C4.
+# --graph) against launched per step (the default), on c3s, C3, C2 and C4;
+# then the Frame.parse step timing.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -15,8 +16,13 @@ run() {   # run NAME WORKLOAD [extra]
   python -c "import json; d=json.load(open('$out')); print('$1 $2', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['verified_bit_exact'], d['config'].get('step'))"
 }
 for i in 1 2; do
-  run graph$i c3s; run launch$i c3s --no-graph
-  run graph$i c3; run launch$i c3 --no-graph
-  run graph$i c2; run launch$i c2 --no-graph
+  run graph$i c3s --graph; run launch$i c3s
+  run graph$i c3 --graph; run launch$i c3
+  run graph$i c2 --graph; run launch$i c2
 done
-run graph1 c4; run launch1 c4 --no-graph
+run graph1 c4 --graph; run launch1 c4
+timeout -k 10 300 python scripts/time_frame_parse.py gpurun_out/ab9_frame_parse.json || exit 1
+# the default bench lines (launched per step, CPU baselines included)
+for w in c3 c3s c2; do
+  timeout -k 10 600 python bench.py --workload $w > gpurun_out/ab9_full_$w.json 2> gpurun_out/ab9_full_$w.err || exit 1
+done

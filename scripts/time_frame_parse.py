@@ -18,7 +18,7 @@ from zstd_decompressor.batch import Plan, run_plan  # noqa: E402
 
 src = gen.text(100_000_000, seed=0x5EED)[:100_000_000]
 data = gen.frames(src, 128 << 10, 3)
-zd.decompress(data[:1 << 20])                     # warm the runtime and caches
+Frame.parse(ForwardByteParser(data)).decode()       # warm the runtime and caches
 
 N = 40
 p = ForwardByteParser(data)
