@@ -2412,9 +2412,6 @@ __device__ inline uint64_t rec_lane(uint64_t raw, int lane) {
 #endif
 constexpr int K4_W = ZD_K4_W;                 // history kept after a slide
 constexpr int K4_B = ZD_K4_B;                 // room kept for a batch (a slide when less is left)
-#ifndef ZD_K4_PACK
-#define ZD_K4_PACK 0                    // the block's symbols and code tables packed (1,636 B of LDS, not 2,048)
-#endif
 #ifndef ZD_K4_C
 #define ZD_K4_C 7200
 #endif
@@ -2755,19 +2752,7 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
   l_u8* const pat = M.pat;
   l_u8* const stg = M.stg;
   const int lane = threadIdx.x & 63;
-#if ZD_K4_PACK
-  // (packed: LL codes 0-35 at 0, ML codes 0-52 at 36; the symbols LL | ML |
-  // OF at 0 / 512 / 1024, OF in 256 entries -- an OF table of AL 9, which
-  // conforming streams never have, is read from its slot in HBM)
-  l_u32* const cl = M.codelut;
-  l_u8* const stb = M.stab;
-  {
-    uint32_t b, e;
-    if (lane < 36) { ll_code((uint32_t)lane, &b, &e); cl[lane] = b | (e << 24); }
-    if (lane < 53) { ml_code((uint32_t)lane, &b, &e); cl[36 + lane] = b | (e << 24); }
-    k4_sync();
-  }
-#elif ZD_K4_CODELUT
+#if ZD_K4_CODELUT
   // LL | ML code -> baseline | extra-bit count << 24 (ll_code / ml_code,
   // sequences.rs tables), one LDS read per code instead of ~20 VALU ops
   l_u32 (*codelut)[64] = (l_u32 (*)[64])M.codelut;
@@ -2864,21 +2849,6 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
     const bool direct = C.seq_direct != 0;
     // the block's LL/OF/ML symbols (K1's sym entries, zd_common.h) -> LDS
     const uint8_t* bsp = src + C.src + CS.bs_off;
-#if ZD_K4_PACK
-    bool ofg = false;                              // OF of AL 9: its symbols from HBM
-    const uint16_t* gof = nullptr;
-    if (n && !direct) {
-      for (int k = 0; k < 3; k++) {
-        const uint32_t s = (uint32_t)C.tab_src[k];
-        const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
-        const int al = cstate[s].al[k];
-        if (k == 1 && al > 8) { ofg = true; gof = g; continue; }
-        l_u8* d = stb + (k == 0 ? 0 : k == 2 ? 512 : 1024);
-        for (int e = lane; e < (1 << al); e += 64) d[e] = (uint8_t)(g[e] & 63);
-      }
-      k4_sync();
-    }
-#else
     if (n && !direct) {
       for (int k = 0; k < 3; k++) {
         const uint32_t s = (uint32_t)C.tab_src[k];
@@ -2888,7 +2858,6 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
       }
       k4_sync();
     }
-#endif
     // Software pipeline over batches of 64 sequences: the records two
     // batches ahead, the bitstream windows of the next batch and its literal
     // bytes (1 KiB from the literal cursor, staged through LDS) one ahead,
@@ -2964,22 +2933,13 @@ __device__ __attribute__((always_inline)) inline void k4_body(const uint8_t* __r
             giant = ofv == DIRECT_GIANT && !C.seq_side;
           } else {
             const uint32_t stt = (uint32_t)(recA >> 32);
-            uint32_t llbase, llb, mlbase, mlb;
-#if ZD_K4_PACK
-            const uint32_t llc = stb[stt & 511], mlc = stb[512 + ((stt >> 10) & 511)];
-            uint32_t ofc;
-            if (ofg) ofc = gof[(stt >> 20) & 511] & 31;
-            else ofc = stb[1024 + ((stt >> 20) & 255)] & 31;
-            const uint32_t cl_ = cl[llc], cm = cl[36 + mlc];
-            llbase = cl_ & 0xFFFFFF; llb = cl_ >> 24;
-            mlbase = cm & 0xFFFFFF; mlb = cm >> 24;
-#elif ZD_K4_CODELUT
             const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
+            uint32_t llbase, llb, mlbase, mlb;
+#if ZD_K4_CODELUT
             const uint32_t cl = codelut[0][llc], cm = codelut[1][mlc];
             llbase = cl & 0xFFFFFF; llb = cl >> 24;
             mlbase = cm & 0xFFFFFF; mlb = cm >> 24;
 #else
-            const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
             ll_code(llc, &llbase, &llb);
             ml_code(mlc, &mlbase, &mlb);
 #endif
@@ -3354,15 +3314,9 @@ __global__ __launch_bounds__(64, ZD_K4_MINW) void zd_k_execute(const uint8_t* __
   // (16 bytes of padding below the window: pass 0 reads up to 15 bytes before a match source)
   __shared__ __attribute__((aligned(16))) uint8_t win[K4_WPAD + K4_C];
   __shared__ __attribute__((aligned(16))) uint8_t pat[64];
-#if ZD_K4_PACK
-  __shared__ __attribute__((aligned(16))) uint8_t stab[2 * FSE_TAB + 256];   // LL | ML | OF symbols of the block
-  __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
-  __shared__ uint32_t codelut[36 + 53];
-#else
   __shared__ __attribute__((aligned(16))) uint8_t stab[3 * FSE_TAB];   // LL | OF | ML symbols of the block
   __shared__ __attribute__((aligned(16))) uint8_t stg[K4_STG + 16];    // a batch's literal bytes (K4_STG of them)
   __shared__ uint32_t codelut[2 * 64];
-#endif
   const K4Lds M{(l_u8*)win + K4_WPAD, (l_u8*)pat, (l_u8*)stab, (l_u8*)stg, (l_u32*)codelut};
   k4_body<false>(src, outbase, frames, fstate, blocks, comp, cstate, lits, seqs, fses, f_begin + blockIdx.x, f_end,
                  gridDim.x, redo, M, nullptr, nullptr);
