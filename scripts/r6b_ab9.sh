@@ -26,3 +26,7 @@ timeout -k 10 300 python scripts/time_frame_parse.py gpurun_out/ab9_frame_parse.
 for w in c3 c3s c2; do
   timeout -k 10 600 python bench.py --workload $w > gpurun_out/ab9_full_$w.json 2> gpurun_out/ab9_full_$w.err || exit 1
 done
+# hops in the sweeps after round 1 (ZD_J_HOPS2; round 1 keeps 6)
+for h in 4 8 12; do
+  ZD_J_HOPS2=$h run hops2_$h c3s
+done
