@@ -1637,8 +1637,10 @@ int zd_decode_async(zd_plan* P, const uint8_t* d_src, uint8_t* d_dst, size_t dst
   // 7 1.76, 8 1.78-1.79, 12 1.85, 16 1.90); ZD_J_HOPS overrides
   static const char* hops_env = getenv("ZD_J_HOPS");
   a.j_hops = one_round ? 1u : hops_env ? (uint32_t)std::max(1, atoi(hops_env)) : 6u;
+  // the sweeps after round 1 (c3s, round 6: 4 / 6 / 8 / 12 hops 3.19 /
+  // 3.09 / 3.08 / 3.06 ms a step, profiles/r6_graph_replay_ab.txt); ZD_J_HOPS2 overrides
   static const char* hops2_env = getenv("ZD_J_HOPS2");
-  a.j_hops2 = one_round ? 1u : hops2_env ? (uint32_t)std::max(1, atoi(hops2_env)) : a.j_hops;
+  a.j_hops2 = one_round ? 1u : hops2_env ? (uint32_t)std::max(1, atoi(hops2_env)) : 12u;
   a.cus = (uint32_t)(k3_slots() / 64);
   a.stream = s;
   // K3 as four lanes per block (K3Q, default): C3 (763 blocks) 2.89 -> 2.31

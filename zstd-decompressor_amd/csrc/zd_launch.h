@@ -26,7 +26,7 @@ struct LaunchArgs {
   bool k3_lat = false;     // K3 as one block per wave (zd_k_sequences_l), few-block plans
   bool k3_quad = true;     // K3 as four lanes per block (zd_k_sequences_q); false: one lane per block
   uint32_t j_hops = 6;                     // K4J: hops per pending word and round (ZD_J_HOPS)
-  uint32_t j_hops2 = 6;                    // K4J: the same in the sweeps after round 1 (ZD_J_HOPS2)
+  uint32_t j_hops2 = 12;                   // K4J: the same in the sweeps after round 1 (ZD_J_HOPS2)
   uint32_t cus = 256;                      // compute units of the device (K4J rounds' grid)
   bool fused = false;                      // K3 + K4 as zd_k_fused, then the redo pass
   bool k1_seq_waves = false;               // K1's sequence half one wave per block (zd_k_tables_seqw)
