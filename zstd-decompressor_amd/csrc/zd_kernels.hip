@@ -1667,6 +1667,18 @@ __device__ inline uint32_t winn_at_tree(const WinN<N>& w, uint32_t y) {
   return __builtin_amdgcn_alignbit(hi, lo, y & 31);
 }
 
+// winn_at for N = 6 by the qword first: the three dwords from 64 (y >> 6) up
+// (two selects each), then lo / hi by bit 5 (one each): 8 selects, not 10,
+// at the same depth (ZD_K3Q_SEL2)
+__device__ inline uint32_t winn_at_q6(const WinN<6>& w, uint32_t y) {
+  const bool q1 = y >= 64, q2 = y >= 128, b0 = (y & 32) != 0;
+  const uint32_t a = q2 ? w.w[4] : (q1 ? w.w[2] : w.w[0]);
+  const uint32_t b = q2 ? w.w[5] : (q1 ? w.w[3] : w.w[1]);
+  const uint32_t c = q2 ? 0u : (q1 ? w.w[4] : w.w[2]);
+  const uint32_t lo = b0 ? b : a, hi = b0 ? c : b;
+  return __builtin_amdgcn_alignbit(hi, lo, y & 31);
+}
+
 // The fast chain: no checks inside the loop.  Each table gives nextState and
 // the step's total bit count for that table (k3f_entry), so a step is
 // pos -= tLL + tML + tOF, then the LL | ML | OF state bits are the low bits
@@ -1870,6 +1882,9 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
+#ifndef ZD_K3Q_SEL2
+#define ZD_K3Q_SEL2 0
+#endif
 #ifndef ZD_K3Q_DEFER
 #define ZD_K3Q_DEFER 0
 #endif
@@ -1947,7 +1962,13 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     const int32_t y = (pos - use.wb) - (int32_t)csum;
     pos -= (int32_t)csum;
     ymin = min(ymin, y);
+#if ZD_K3Q_SEL2
+    uint32_t r;
+    if constexpr (N == 6) r = winn_at_q6(use, (uint32_t)y);
+    else r = winn_at_tree<N>(use, (uint32_t)y);
+#else
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
+#endif
 #if ZD_K3Q_DEFER
     pend = pos;
 #else
