@@ -4276,21 +4276,8 @@ __device__ inline void j_scan_map(uint64_t m[3], int lane) {
 }
 
 // The block's LL/OF/ML symbols (K1's sym entries) -> LDS.
-// (and the LL | ML code tables, as K4's codelut: baseline | extra bits << 24;
-// ZD_J_CODELUT 0: the codes decoded by ll_code / ml_code, the round-5 form)
-#ifndef ZD_J_CODELUT
-#define ZD_J_CODELUT 1
-#endif
-__device__ inline void j_stab(uint8_t (*stab)[FSE_TAB], uint32_t* jcl, const CompBlock& C,
-                              const CompBlock* __restrict__ comp, const CompState* __restrict__ cstate,
-                              const uint16_t* __restrict__ fses, int lane) {
-  {
-    uint32_t b, e;
-    ll_code((uint32_t)lane, &b, &e);
-    jcl[lane] = b | (e << 24);
-    ml_code((uint32_t)lane, &b, &e);
-    jcl[64 + lane] = b | (e << 24);
-  }
+__device__ inline void j_stab(uint8_t (*stab)[FSE_TAB], const CompBlock& C, const CompBlock* __restrict__ comp,
+                              const CompState* __restrict__ cstate, const uint16_t* __restrict__ fses, int lane) {
   for (int k = 0; k < 3; k++) {
     const uint32_t s = (uint32_t)C.tab_src[k];
     const uint16_t* g = fses + (uint64_t)comp[s].fse_slot * FSE_SLOT + k * FSE_TAB;
@@ -4302,18 +4289,13 @@ __device__ inline void j_stab(uint8_t (*stab)[FSE_TAB], uint32_t* jcl, const Com
 
 // update_symbol_value (decoders/sequence.rs:41-55) from a K3 record: OF, ML,
 // LL extra bits below the recorded position, in that order.
-__device__ inline void j_values(uint64_t rec, const WinU& w, const uint8_t (*stab)[FSE_TAB], const uint32_t* jcl,
-                                uint32_t& ll, uint32_t& ml, uint32_t& ofv) {
+__device__ inline void j_values(uint64_t rec, const WinU& w, const uint8_t (*stab)[FSE_TAB], uint32_t& ll,
+                                uint32_t& ml, uint32_t& ofv) {
   const uint32_t stt = (uint32_t)(rec >> 32);
   const uint32_t llc = stab[0][stt & 1023], mlc = stab[2][(stt >> 10) & 1023], ofc = stab[1][stt >> 20] & 31;
-#if ZD_J_CODELUT
-  const uint32_t cl = jcl[llc & 63], cm = jcl[64 + (mlc & 63)];
-  const uint32_t llbase = cl & 0xFFFFFF, llb = cl >> 24, mlbase = cm & 0xFFFFFF, mlb = cm >> 24;
-#else
   uint32_t llbase, llb, mlbase, mlb;
   ll_code(llc, &llbase, &llb);
   ml_code(mlc, &mlbase, &mlb);
-#endif
   uint64_t t = winu_top(w, 0);
   const uint32_t ob = take_top(t, ofc), mb = take_top(t, mlb), lb = take_top(t, llb);
   ofv = (1u << ofc) + ob;
@@ -4419,7 +4401,6 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
                                                 const JBlkDesc* __restrict__ jd, const JSegDesc* __restrict__ jsd,
                                                 JSeg* __restrict__ jseg) {
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
-  __shared__ uint32_t jcl[128];                  // LL | ML code tables (j_stab)
   const int lane = threadIdx.x;
   const JSegDesc SD = jsd[blockIdx.x];
   const JBlkDesc D = jd[SD.jblk];
@@ -4434,13 +4415,13 @@ __global__ __launch_bounds__(64) void zd_k_jsum(const uint8_t* __restrict__ src,
     const CompBlock C = comp[B.comp];
     const uint32_t n = C.nseq, sb = SD.k * J_SEG, se = min(n, sb + J_SEG);
     if (!CS.stop && se > sb) {
-      j_stab(stab, jcl, C, comp, cstate, fses, lane);
+      j_stab(stab, C, comp, cstate, fses, lane);
       JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, se, C.seq_direct != 0};
       R.start(sb, lane);
       for (uint32_t s0 = sb; s0 < se; s0 += 64) {
         const int k = (int)min(64u, se - s0);
         uint32_t ll = 0, ml = 0, ofv = 4;
-        if (lane < k) j_values(R.recA, R.winA, stab, jcl, ll, ml, ofv);
+        if (lane < k) j_values(R.recA, R.winA, stab, ll, ml, ofv);
         R.next(s0, lane);
         int bl, bc;
         (void)j_offsets<true>(ofv, ll, k, rep, &bl, &bc);
@@ -4624,7 +4605,6 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
                                                     const JSeg* __restrict__ jseg, const JSegDesc* __restrict__ jsd,
                                                     uint32_t* jst) {
   __shared__ __attribute__((aligned(16))) uint8_t stab[3][FSE_TAB];
-  __shared__ uint32_t jcl[128];                  // LL | ML code tables (j_stab)
   __shared__ uint32_t sa[65], sll[64], soff[64], slp[64];
 #if ZD_JS_STAGE
   __shared__ __attribute__((aligned(16))) uint8_t slit_[JS_STG];
@@ -4658,14 +4638,14 @@ __global__ __launch_bounds__(64) void zd_k_jscatter(const uint8_t* __restrict__ 
   const uint32_t n = C.nseq;
   const uint32_t sb = SD.k * J_SEG, se = min(n, sb + J_SEG);
   if (se > sb) {
-    j_stab(stab, jcl, C, comp, cstate, fses, lane);
+    j_stab(stab, C, comp, cstate, fses, lane);
     JRecs R{seqs + C.seq_out, src + C.src + CS.bs_off, (uintptr_t)src, se, C.seq_direct != 0};
     R.start(sb, lane);
     for (uint32_t s0 = sb; s0 < se; s0 += 64) {
       const int k = (int)min(64u, se - s0);
       const bool valid = lane < k;
       uint32_t ll = 0, ml = 0, ofv = 4;
-      if (valid) j_values(R.recA, R.winA, stab, jcl, ll, ml, ofv);
+      if (valid) j_values(R.recA, R.winA, stab, ll, ml, ofv);
       R.next(s0, lane);
       int bl, bc;
       const uint64_t off = j_offsets<false>(ofv, ll, k, rep, &bl, &bc);
