@@ -1670,13 +1670,22 @@ __device__ inline uint32_t winn_at_tree(const WinN<N>& w, uint32_t y) {
 // winn_at for N = 6 by the qword first: the three dwords from 64 (y >> 6) up
 // (two selects each), then lo / hi by bit 5 (one each): 8 selects, not 10,
 // at the same depth (ZD_K3Q_SEL2)
-__device__ inline uint32_t winn_at_q6(const WinN<6>& w, uint32_t y) {
-  const bool q1 = y >= 64, q2 = y >= 128, b0 = (y & 32) != 0;
-  const uint32_t a = q2 ? w.w[4] : (q1 ? w.w[2] : w.w[0]);
-  const uint32_t b = q2 ? w.w[5] : (q1 ? w.w[3] : w.w[1]);
-  const uint32_t c = q2 ? 0u : (q1 ? w.w[4] : w.w[2]);
-  const uint32_t lo = b0 ? b : a, hi = b0 ? c : b;
-  return __builtin_amdgcn_alignbit(hi, lo, y & 31);
+// (the selects as v_cndmask in inline asm on ballot masks: written as C
+// ternaries, the compiler turned them into a dynamic index of the window
+// array, which it then kept in scratch)
+__device__ inline uint32_t sel_m(uint64_t m, uint32_t f, uint32_t t) {   // lane in m ? t : f
+  uint32_t r;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+template <int N>
+__device__ inline uint32_t winn_at_q6(const WinN<N>& w, uint32_t y) {
+  static_assert(N == 6, "qword-first select for 6-dword windows");
+  const uint64_t q1 = __ballot(y >= 64), q2 = __ballot(y >= 128), b0 = __ballot((y & 32) != 0);
+  const uint32_t a = sel_m(q2, sel_m(q1, w.w[0], w.w[2]), w.w[4]);
+  const uint32_t b = sel_m(q2, sel_m(q1, w.w[1], w.w[3]), w.w[5]);
+  const uint32_t c = sel_m(q2, sel_m(q1, w.w[2], w.w[4]), 0u);
+  return __builtin_amdgcn_alignbit(sel_m(b0, b, c), sel_m(b0, a, b), y & 31);
 }
 
 // The fast chain: no checks inside the loop.  Each table gives nextState and
@@ -1963,9 +1972,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     pos -= (int32_t)csum;
     ymin = min(ymin, y);
 #if ZD_K3Q_SEL2
-    uint32_t r;
-    if constexpr (N == 6) r = winn_at_q6(use, (uint32_t)y);
-    else r = winn_at_tree<N>(use, (uint32_t)y);
+    const uint32_t r = winn_at_q6<N>(use, (uint32_t)y);
 #else
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
 #endif
