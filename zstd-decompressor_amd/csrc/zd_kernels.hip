@@ -1667,27 +1667,6 @@ __device__ inline uint32_t winn_at_tree(const WinN<N>& w, uint32_t y) {
   return __builtin_amdgcn_alignbit(hi, lo, y & 31);
 }
 
-// winn_at for N = 6 by the qword first: the three dwords from 64 (y >> 6) up
-// (two selects each), then lo / hi by bit 5 (one each): 8 selects, not 10,
-// at the same depth (ZD_K3Q_SEL2)
-// (the selects as v_cndmask in inline asm on ballot masks: written as C
-// ternaries, the compiler turned them into a dynamic index of the window
-// array, which it then kept in scratch)
-__device__ inline uint32_t sel_m(uint64_t m, uint32_t f, uint32_t t) {   // lane in m ? t : f
-  uint32_t r;
-  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
-  return r;
-}
-template <int N>
-__device__ inline uint32_t winn_at_q6(const WinN<N>& w, uint32_t y) {
-  static_assert(N == 6, "qword-first select for 6-dword windows");
-  const uint64_t q1 = __ballot(y >= 64), q2 = __ballot(y >= 128), b0 = __ballot((y & 32) != 0);
-  const uint32_t a = sel_m(q2, sel_m(q1, w.w[0], w.w[2]), w.w[4]);
-  const uint32_t b = sel_m(q2, sel_m(q1, w.w[1], w.w[3]), w.w[5]);
-  const uint32_t c = sel_m(q2, sel_m(q1, w.w[2], w.w[4]), 0u);
-  return __builtin_amdgcn_alignbit(sel_m(b0, b, c), sel_m(b0, a, b), y & 31);
-}
-
 // The fast chain: no checks inside the loop.  Each table gives nextState and
 // the step's total bit count for that table (k3f_entry), so a step is
 // pos -= tLL + tML + tOF, then the LL | ML | OF state bits are the low bits
@@ -1891,9 +1870,6 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
-#ifndef ZD_K3Q_SEL2
-#define ZD_K3Q_SEL2 0
-#endif
 #ifndef ZD_K3Q_DEFER
 #define ZD_K3Q_DEFER 0
 #endif
@@ -1971,11 +1947,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     const int32_t y = (pos - use.wb) - (int32_t)csum;
     pos -= (int32_t)csum;
     ymin = min(ymin, y);
-#if ZD_K3Q_SEL2
-    const uint32_t r = winn_at_q6<N>(use, (uint32_t)y);
-#else
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
-#endif
 #if ZD_K3Q_DEFER
     pend = pos;
 #else
