@@ -1870,9 +1870,6 @@ __device__ inline uint32_t quad_max(uint32_t x) {
 // 16-record lines of `out` whose stores have completed (a line eight pairs
 // back: vmcnt(32) leaves the newer window loads and stores in flight), for
 // the K4 wave of its workgroup.
-#ifndef ZD_K3Q_DEFER
-#define ZD_K3Q_DEFER 0
-#endif
 template <int L, int N, bool PUB = false>
 __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, const lds_u16* tab, int role,
                           int all, int alo, int alm, uint32_t n, uint64_t* __restrict__ out,
@@ -1923,20 +1920,8 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   }
   uint32_t mx = 0;
   int32_t ymin = 0;
-#if ZD_K3Q_DEFER
-  // ZD_K3Q_DEFER: a step's window load (for the step L on) is issued by the
-  // next step, after that step's table read, so the two VMEM issues stay off
-  // the path from the state to its table read.  pend: the position the load
-  // anchors at (the first step reloads w[L - 1] at its own anchor, a no-op)
-  int32_t pend = pos;
-  auto step = [&](WinN<N>& use, WinN<N>& prev) {
-    const uint32_t e = tab[s];
-    asm volatile("" ::: "memory");
-    prev = winn_load<N>(bs, m, pend);
-#else
   auto step = [&](WinN<N>& use) {
     const uint32_t e = tab[s];
-#endif
     mx = max(mx, e);                                // (the shadow lane's e is the LL lane's)
     const uint32_t ns = e & 1023, nb = __builtin_clz(ns) + ar;
     // the three roles' counts by three quad broadcasts and one add3 (the
@@ -1948,11 +1933,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
     pos -= (int32_t)csum;
     ymin = min(ymin, y);
     const uint32_t r = winn_at_tree<N>(use, (uint32_t)y);   // (linear select: C3 K3 2.21 ms, tree 2.06)
-#if ZD_K3Q_DEFER
-    pend = pos;
-#else
     use = winn_load<N>(bs, m, pos);
-#endif
     // the state bits sit OF | ML | LL upwards from y: offsets 0, nbO, nbO +
     // nbM (the shadow takes the LL lane's), by quad_perm [0,0,1,1] twice
     const uint32_t t = qdpp<0x50>(nb) & m0;
@@ -1966,11 +1947,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
   for (; i + 1 < n; i += U) {
 #pragma unroll
     for (int k = 0; k < U; k += 2) {
-#if ZD_K3Q_DEFER
-      step(w[k % L], w[(k + L - 1) % L]);
-#else
       step(w[k % L]);
-#endif
       asm volatile("" ::: "memory");
       const uint32_t slot = i + k;                  // pair (i + k, i + k + 1)
       if constexpr (U == 4) {
@@ -1992,11 +1969,7 @@ __device__ int seq_chainq(const uint8_t* bs, uint32_t bs_size, uintptr_t base, c
           if (role == 0) *prog = (slot + 2 - 16) >> 4;
         }
       }
-#if ZD_K3Q_DEFER
-      step(w[(k + 1) % L], w[k % L]);
-#else
       step(w[(k + 1) % L]);
-#endif
       pS = s;
       pPos = (uint32_t)pos;
     }
