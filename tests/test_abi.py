@@ -106,3 +106,19 @@ def test_frame_parse_headers(kat):
         f = Frame.parse(ForwardByteParser(data))
         h = f.inner.header()
         assert (h.window_size, h.content_size, h.dictionnary_id) == (c["window"], c["fcs"], c["dict"]), c["src"]
+
+
+def test_buf_from_points_into_the_bytes():
+    """_lib.buf_from (Frame.parse's remaining bytes, no slice copy): the
+    pointer is the bytes' own buffer at the offset."""
+    import ctypes as C
+    from zstd_decompressor import _lib
+    data = bytes(range(256)) * 17
+    for off in (0, 1, 255, len(data) - 1, len(data)):
+        p, n, keep = _lib.buf_from(data, off)
+        assert n == max(len(data) - off, 0)
+        if n:
+            assert C.string_at(p, n) == data[off:]
+            base, _, _ = _lib.buf(data)
+            assert p.value == base.value + off
+
