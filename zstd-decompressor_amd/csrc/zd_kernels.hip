@@ -3324,6 +3324,7 @@ struct FzK1 {
   uint16_t cum[260];                 // placements before each symbol
   uint16_t cnt[256];                 // nextState counters
   uint8_t sym[FSE_TAB];
+  uint64_t lanes[64];                // fz_build_fse: a chunk's lanes by symbol (tables of <= 64 symbols)
 };
 struct FzInfo {                      // a block's table results, for wave 0
   uint32_t al;                       // LL | OF << 8 | ML << 16
@@ -3343,6 +3344,9 @@ __device__ inline uint32_t lanes_below(uint64_t m) {
 // symbol from the placement's rank (a search over the cumulative counts).
 // nextState of state i is count(s) plus the earlier states of s: per 64
 // states, one round per distinct symbol.
+#ifndef ZD_FZ_LANEMASK
+#define ZD_FZ_LANEMASK 1
+#endif
 __device__ int fz_build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t* tab, FzK1& W, int lane) {
   if (al > FSE_MAX_AL) return ZD_E_LARGE_ACCURACY_LOG;
   const uint32_t T = 1u << al, mask = T - 1, step = (T >> 1) + (T >> 3) + 3;
@@ -3388,18 +3392,32 @@ __device__ int fz_build_fse(int al, const int16_t* dist, uint32_t nsym, uint16_t
     W.cnt[s] = (uint16_t)(c > 0 ? c : (c == -1 ? 1 : 0));
   }
   k4_sync();
+  const bool by_lds = ZD_FZ_LANEMASK && nsym <= 64;
   for (uint32_t i0 = 0; i0 < T; i0 += 64) {
     const uint32_t i = i0 + lane;
     const uint32_t s = i < T ? W.sym[i] : 0u;
-    // the lane's rank among the chunk's states of its symbol, and their
-    // number (registers only: one round per distinct symbol)
-    uint64_t rem = __ballot(i < T);
+    // the lane's rank among the chunk's states of its symbol, and their number
     uint32_t occ = 0, tot = 0;
-    while (rem) {
-      const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)__builtin_ctzll(rem));
-      const uint64_t m = __ballot(s == sl) & rem;
-      if ((m >> lane) & 1) { occ = lanes_below(m); tot = (uint32_t)__popcll(m); }
-      rem &= ~m;
+    if (by_lds) {
+      // the chunk's lanes of each symbol as a 64-bit mask in LDS (one OR
+      // per lane), instead of one ballot round per distinct symbol (C3: the
+      // three tables took ~31 us)
+      if (i < T) W.lanes[s] = 0;
+      k4_sync();
+      if (i < T) __hip_atomic_fetch_or(&W.lanes[s], 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      k4_sync();
+      const uint64_t m = i < T ? W.lanes[s] : 0ull;
+      occ = lanes_below(m);
+      tot = (uint32_t)__popcll(m);
+    } else {
+      // (registers only: one round per distinct symbol)
+      uint64_t rem = __ballot(i < T);
+      while (rem) {
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)s, (int)__builtin_ctzll(rem));
+        const uint64_t m = __ballot(s == sl) & rem;
+        if ((m >> lane) & 1) { occ = lanes_below(m); tot = (uint32_t)__popcll(m); }
+        rem &= ~m;
+      }
     }
     const uint32_t ns = i < T ? W.cnt[s] + occ : 0u;
     k4_sync();
