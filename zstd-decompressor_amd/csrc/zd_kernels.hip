@@ -164,6 +164,9 @@ constexpr uint32_t K1S_SYMS = 64;
 // from a 4-aligned base on lane i % 64 of r[i / 64]; FwBits' 64-bit cache
 // refilled by two readlanes instead of a dependent memory load (past the
 // 512 bytes held: memory).  The wave runs it on uniform values.
+#ifndef ZD_FWW32
+#define ZD_FWW32 1
+#endif
 struct FwBitsW {
   const uint8_t* d;
   uint32_t nbytes;
@@ -171,10 +174,19 @@ struct FwBitsW {
   uint32_t r0, r1;
   uint32_t delta;                                  // bit of the register base where d starts
   uint64_t cache = 0;
+#if ZD_FWW32
+  // (32-bit bookkeeping: a description is < 2^28 bits past the register base;
+  // the 64-bit compares cost the serial walk several SALU ops each)
+  int32_t cbit = -1;                               // register-base bit of cache bit 0 (-1: empty)
+  __device__ inline uint32_t bits(uint32_t at, int len) {   // len <= 24, within range
+    const int32_t a = (int32_t)(at + delta);
+    if (cbit < 0 || a < cbit || a + len > cbit + 64) {
+#else
   int64_t cbit = -1;                               // register-base bit of cache bit 0 (-1: empty)
   __device__ inline uint32_t bits(uint32_t at, int len) {   // len <= 24, within range
     const uint32_t a = at + delta;
     if (cbit < 0 || (int64_t)a < cbit || (int64_t)a + len > cbit + 64) {
+#endif
       const uint32_t w = a >> 5;
       if (w + 1 < 128) {
         const uint32_t lo = (uint32_t)(w < 64 ? __builtin_amdgcn_readlane((int)r0, (int)w)
@@ -185,10 +197,10 @@ struct FwBitsW {
         cbit = (int64_t)w * 32;
       } else {
         cache = load_u64(d + (at >> 3), d, d + nbytes);
-        cbit = (int64_t)delta + (int64_t)(at >> 3) * 8;
+        cbit = (int32_t)delta + (int32_t)(at >> 3) * 8;
       }
     }
-    return (uint32_t)(cache >> ((int64_t)a - cbit)) & ((1u << len) - 1);
+    return (uint32_t)(cache >> (a - cbit)) & ((1u << len) - 1);
   }
   __device__ inline int peek(int len, uint32_t* v) {
     if ((int64_t)nbytes * 8 - pos < len) return ZD_E_NOT_ENOUGH_BITS;
