@@ -203,7 +203,11 @@ struct FwBitsW {
     return (uint32_t)(cache >> (a - cbit)) & ((1u << len) - 1);
   }
   __device__ inline int peek(int len, uint32_t* v) {
+#if ZD_FWW32
+    if ((int32_t)(nbytes * 8) - (int32_t)pos < len) return ZD_E_NOT_ENOUGH_BITS;   // (nbytes: within a block)
+#else
     if ((int64_t)nbytes * 8 - pos < len) return ZD_E_NOT_ENOUGH_BITS;
+#endif
     *v = len ? bits(pos, len) : 0;
     return 0;
   }
