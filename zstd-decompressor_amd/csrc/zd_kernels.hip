@@ -164,9 +164,6 @@ constexpr uint32_t K1S_SYMS = 64;
 // from a 4-aligned base on lane i % 64 of r[i / 64]; FwBits' 64-bit cache
 // refilled by two readlanes instead of a dependent memory load (past the
 // 512 bytes held: memory).  The wave runs it on uniform values.
-#ifndef ZD_FWW32
-#define ZD_FWW32 1
-#endif
 struct FwBitsW {
   const uint8_t* d;
   uint32_t nbytes;
@@ -174,19 +171,12 @@ struct FwBitsW {
   uint32_t r0, r1;
   uint32_t delta;                                  // bit of the register base where d starts
   uint64_t cache = 0;
-#if ZD_FWW32
-  // (32-bit bookkeeping: a description is < 2^28 bits past the register base;
-  // the 64-bit compares cost the serial walk several SALU ops each)
+  // (32-bit bookkeeping: a description lies within its block, < 2^24 bits
+  // past the register base; 64-bit compares cost the serial walk SALU ops)
   int32_t cbit = -1;                               // register-base bit of cache bit 0 (-1: empty)
   __device__ inline uint32_t bits(uint32_t at, int len) {   // len <= 24, within range
     const int32_t a = (int32_t)(at + delta);
     if (cbit < 0 || a < cbit || a + len > cbit + 64) {
-#else
-  int64_t cbit = -1;                               // register-base bit of cache bit 0 (-1: empty)
-  __device__ inline uint32_t bits(uint32_t at, int len) {   // len <= 24, within range
-    const uint32_t a = at + delta;
-    if (cbit < 0 || (int64_t)a < cbit || (int64_t)a + len > cbit + 64) {
-#endif
       const uint32_t w = a >> 5;
       if (w + 1 < 128) {
         const uint32_t lo = (uint32_t)(w < 64 ? __builtin_amdgcn_readlane((int)r0, (int)w)
@@ -203,11 +193,7 @@ struct FwBitsW {
     return (uint32_t)(cache >> (a - cbit)) & ((1u << len) - 1);
   }
   __device__ inline int peek(int len, uint32_t* v) {
-#if ZD_FWW32
-    if ((int32_t)(nbytes * 8) - (int32_t)pos < len) return ZD_E_NOT_ENOUGH_BITS;   // (nbytes: within a block)
-#else
-    if ((int64_t)nbytes * 8 - pos < len) return ZD_E_NOT_ENOUGH_BITS;
-#endif
+    if ((int32_t)(nbytes * 8) - (int32_t)pos < len) return ZD_E_NOT_ENOUGH_BITS;
     *v = len ? bits(pos, len) : 0;
     return 0;
   }
@@ -4488,15 +4474,25 @@ __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__
   uint64_t pos = 0;
   uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
   bool stop = false;
+  // the next chunk's blocks are loaded while this one's scans run
+  struct Ld { uint64_t size, m0, m1, m2; uint32_t dead; };
+  auto load = [&](uint32_t c) -> Ld {
+    const uint32_t e = JF.jb0 + c + lane;
+    if (c + lane >= JF.njb) return Ld{0, jr_sym(0), jr_sym(1), jr_sym(2), 1u};
+    return Ld{jb[e].size, jb[e].map[0], jb[e].map[1], jb[e].map[2], jb[e].dead};
+  };
+  Ld nx = load(0);
   for (uint32_t c = 0; c < JF.njb; c += 64) {
     const uint32_t e = JF.jb0 + c + lane;
     const bool v = c + lane < JF.njb;
+    const Ld cur = nx;
+    if (c + 64 < JF.njb) nx = load(c + 64);
     uint64_t size = 0, m[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
     uint32_t dead = 1;
     if (v && !stop) {
-      size = jb[e].size;
-      m[0] = jb[e].map[0]; m[1] = jb[e].map[1]; m[2] = jb[e].map[2];
-      dead = jb[e].dead;
+      size = cur.size;
+      m[0] = cur.m0; m[1] = cur.m1; m[2] = cur.m2;
+      dead = cur.dead;
     }
     // blocks from the first dead one on do not run
     const uint64_t dm = __ballot(v && dead);
