@@ -4443,9 +4443,11 @@ __global__ __launch_bounds__(64) void zd_k_jsum_blocks(const FrameState* __restr
       const uint32_t nseg = C.nseq > J_SEG ? (C.nseq + J_SEG - 1) / J_SEG : 1;
       uint64_t out = 0;
       uint32_t lit = 0;
+      JSeg tn = jseg[D.seg0];                       // (the next segment's sums loaded a step ahead)
       for (uint32_t k = 0; k < nseg; k++) {
         JSeg& g = jseg[D.seg0 + k];
-        const JSeg t = g;                           // the segment's own sums
+        const JSeg t = tn;                          // the segment's own sums
+        if (k + 1 < nseg) tn = jseg[D.seg0 + k + 1];
         g.out_rel = out;
         g.lit_rel = lit;
         g.map[0] = map[0]; g.map[1] = map[1]; g.map[2] = map[2];
