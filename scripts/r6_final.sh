@@ -13,4 +13,6 @@ echo "smoke rc=$rc"; tail -1 gpurun_out/fin_smoke.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > gpurun_out/fin_c4.json 2> gpurun_out/fin_c4.err || exit 1
 timeout -k 10 600 python bench.py --workload c3s > gpurun_out/fin_c3s.json 2> gpurun_out/fin_c3s.err || exit 1
-for w in c4 c3s; do python -c "import json; d=json.load(open('gpurun_out/fin_$w.json')); print('$w', d['value'], d['ms_per_step'], d['roofline']['kernel'][:30], d['roofline']['kernel_ms'], d['roofline']['frac'], d['verified_bit_exact'], d['cpu_baseline']['value'])"; done
+timeout -k 10 600 python bench.py --workload c3 > gpurun_out/fin_c3.json 2> gpurun_out/fin_c3.err || exit 1
+timeout -k 10 600 python bench.py --workload c2 > gpurun_out/fin_c2.json 2> gpurun_out/fin_c2.err || exit 1
+for w in c4 c3s c3 c2; do python -c "import json; d=json.load(open('gpurun_out/fin_$w.json')); print('$w', d['value'], d['ms_per_step'], d['roofline']['kernel'][:30], d['roofline']['kernel_ms'], d['roofline']['frac'], d['verified_bit_exact'], d['cpu_baseline']['value'])"; done
