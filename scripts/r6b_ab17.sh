@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-6 check 17: zd_k_jprefix as one workgroup of 16 waves a frame (the waves' scans
+# composed by one lane, a serial fallback from a super-chunk with a dead or over-capacity block) -- K4J
+# parity, c3s lines, and the c3s kernel stats of the same build.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp ZD_CORPUS_CACHE=/tmp/zdc
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_large_frames.py \
+  tests/test_fuzz.py "tests/test_gpu_parity.py::test_resources" "tests/test_gpu_parity.py::test_fused_table_builds" \
+  "tests/test_gpu_parity.py::test_out_of_domain_triggers" "tests/test_gpu_parity.py::test_synthetic_multi_block_frames" "tests/test_gpu_parity.py::test_corrupted_inputs" "tests/test_gpu_parity.py::test_multi_block_frames_forked_plan" "tests/test_gpu_parity.py::test_context_block_by_block" "tests/test_gpu_parity.py::test_hip_graph_capture_replay" -m gpu > gpurun_out/ab17_pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 gpurun_out/ab17_pytest.log
+[ $rc -eq 0 ] || exit $rc
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --workload c3s --no-cpu-baseline --no-host-io > gpurun_out/ab17_c3s_$i.json 2> gpurun_out/ab17_c3s_$i.err || exit 1
+  python -c "import json; d=json.load(open('gpurun_out/ab17_c3s_$i.json')); print('c3s', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['verified_bit_exact'])"
+done
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/ab17_prof_c3s -o run --output-format csv -- python bench.py --workload c3s --no-cpu-baseline --no-host-io > gpurun_out/ab17_prof.json 2> gpurun_out/ab17_prof.err || exit 1
+python - <<'PY'
+import csv, glob
+f = glob.glob('gpurun_out/ab17_prof_c3s/**/*kernel_stats.csv', recursive=True)[0]
+for r in csv.reader(open(f)):
+    if r[0] != 'Name' and float(r[3]) > 10000:
+        print(f"{r[0].split('(')[0][:45]:45s} {r[1]:>5s} {float(r[3])/1e3:9.1f} us")
+PY

@@ -4466,15 +4466,13 @@ __global__ __launch_bounds__(64) void zd_k_jsum_blocks(const FrameState* __restr
   jb[e].dead = dead;
 }
 
-__global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__ frames, FrameState* fstate,
-                                                   const JFrame* __restrict__ jframes, const JBlkDesc* __restrict__ jd,
-                                                   JBlk* jb) {
-  const int lane = threadIdx.x;
-  const JFrame JF = jframes[blockIdx.x];
-  const uint64_t cap = frames[JF.frame].out_cap;
-  FrameState* S = &fstate[JF.frame];
-  uint64_t pos = 0;
-  uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
+// The frame's blocks one 64-block chunk after another from block c_start,
+// entering (pos, rep): a dead block (a failure before it) or one past the
+// frame's capacity stops the frame there.  One wave; writes the frame's
+// outcome to S.
+__device__ inline void jp_serial(const JFrame& JF, uint64_t cap, FrameState* S, FrameState* fstate,
+                                 const JBlkDesc* __restrict__ jd, JBlk* jb, uint32_t c_start, uint64_t pos,
+                                 uint64_t rep[3], int lane) {
   bool stop = false;
   // the next chunk's blocks are loaded while this one's scans run
   struct Ld { uint64_t size, m0, m1, m2; uint32_t dead; };
@@ -4483,8 +4481,8 @@ __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__
     if (c + lane >= JF.njb) return Ld{0, jr_sym(0), jr_sym(1), jr_sym(2), 1u};
     return Ld{jb[e].size, jb[e].map[0], jb[e].map[1], jb[e].map[2], jb[e].dead};
   };
-  Ld nx = load(0);
-  for (uint32_t c = 0; c < JF.njb; c += 64) {
+  Ld nx = load(c_start);
+  for (uint32_t c = c_start; c < JF.njb; c += 64) {
     const uint32_t e = JF.jb0 + c + lane;
     const bool v = c + lane < JF.njb;
     const Ld cur = nx;
@@ -4529,6 +4527,88 @@ __global__ __launch_bounds__(64) void zd_k_jprefix(const FrameDesc* __restrict__
     if (fd < 64 || om) stop = true;
   }
   if (lane == 0) {
+    S->out_len = pos;
+    S->rep[0] = rep[0];
+    S->rep[1] = rep[1];
+    S->rep[2] = rep[2];
+  }
+}
+
+// KJ2: one workgroup of JP_WAVES waves per frame.  Blocks in super-chunks of
+// 64 x JP_WAVES: each wave scans its 64 blocks' sizes and repeat-offset maps,
+// one lane composes the waves' totals in order, and every block gets its
+// output start and entering offsets at once (c3s: the one-wave loop over 12
+// chunks took ~22 us).  A super-chunk with a dead block or a block past the
+// frame's capacity goes to jp_serial from its start (the same outcome).
+constexpr int JP_WAVES = 16;
+__global__ __launch_bounds__(64 * JP_WAVES) void zd_k_jprefix(const FrameDesc* __restrict__ frames, FrameState* fstate,
+                                                              const JFrame* __restrict__ jframes,
+                                                              const JBlkDesc* __restrict__ jd, JBlk* jb) {
+  __shared__ uint64_t wsz[JP_WAVES], wmap[JP_WAVES][3], wpos[JP_WAVES + 1], wrep[JP_WAVES + 1][3];
+  __shared__ uint32_t flag;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const JFrame JF = jframes[blockIdx.x];
+  const uint64_t cap = frames[JF.frame].out_cap;
+  FrameState* S = &fstate[JF.frame];
+  uint64_t pos = 0;
+  uint64_t rep[3] = {S->rep[0], S->rep[1], S->rep[2]};
+  uint32_t c0 = 0;
+  for (; c0 < JF.njb; c0 += 64 * JP_WAVES) {
+    const uint32_t i = c0 + (uint32_t)t, e = JF.jb0 + i;
+    const bool v = i < JF.njb;
+    uint64_t size = 0, m[3] = {jr_sym(0), jr_sym(1), jr_sym(2)};
+    uint32_t dead = 0;
+    if (v) {
+      size = jb[e].size;
+      m[0] = jb[e].map[0]; m[1] = jb[e].map[1]; m[2] = jb[e].map[2];
+      dead = jb[e].dead;
+    }
+    if (t == 0) flag = 0;
+    __syncthreads();
+    if (v && dead) flag = 1;
+    const uint64_t incl = wave_scan_u64(size, lane);
+    j_scan_map(m, lane);                           // m: the wave's inclusive composites
+    if (lane == 63) {
+      wsz[wv] = incl;
+      wmap[wv][0] = m[0]; wmap[wv][1] = m[1]; wmap[wv][2] = m[2];
+    }
+    __syncthreads();
+    if (t == 0) {                                  // the waves' entering states, in order
+      uint64_t p = pos, r0 = rep[0], r1 = rep[1], r2 = rep[2];
+      for (int w = 0; w < JP_WAVES; w++) {
+        wpos[w] = p;
+        wrep[w][0] = r0; wrep[w][1] = r1; wrep[w][2] = r2;
+        p += wsz[w];
+        const uint64_t r[3] = {r0, r1, r2};
+        r0 = jr_apply(wmap[w][0], r); r1 = jr_apply(wmap[w][1], r); r2 = jr_apply(wmap[w][2], r);
+      }
+      wpos[JP_WAVES] = p;
+      wrep[JP_WAVES][0] = r0; wrep[JP_WAVES][1] = r1; wrep[JP_WAVES][2] = r2;
+    }
+    __syncthreads();
+    const uint64_t wp = wpos[wv];
+    const uint64_t wr[3] = {wrep[wv][0], wrep[wv][1], wrep[wv][2]};
+    if (v && wp + incl > cap) flag = 1;            // past the frame's capacity
+    __syncthreads();
+    if (flag) break;                               // (uniform: read after the barrier)
+    uint64_t ex[3] = {shfl_up_u64(m[0], 1), shfl_up_u64(m[1], 1), shfl_up_u64(m[2], 1)};
+    if (lane == 0) { ex[0] = jr_sym(0); ex[1] = jr_sym(1); ex[2] = jr_sym(2); }
+    if (v) {
+      jb[e].out_start = wp + incl - size;
+      jb[e].rep_in[0] = jr_apply(ex[0], wr);
+      jb[e].rep_in[1] = jr_apply(ex[1], wr);
+      jb[e].rep_in[2] = jr_apply(ex[2], wr);
+      jb[e].dead = 0;
+    }
+    pos = wpos[JP_WAVES];
+    rep[0] = wrep[JP_WAVES][0]; rep[1] = wrep[JP_WAVES][1]; rep[2] = wrep[JP_WAVES][2];
+    __syncthreads();                               // (the LDS totals are rewritten next)
+  }
+  if (c0 < JF.njb) {                               // a dead or over-capacity block in this super-chunk
+    if (wv == 0) jp_serial(JF, cap, S, fstate, jd, jb, c0, pos, rep, lane);
+    return;
+  }
+  if (t == 0) {
     S->out_len = pos;
     S->rep[0] = rep[0];
     S->rep[1] = rep[1];
@@ -5177,7 +5257,7 @@ hipError_t launch_pipeline(const LaunchArgs& a) {
                        (const CompState*)cstate, (const uint64_t*)seqs, (const uint16_t*)fses, jframes, jd, jsd, jseg);
     hipLaunchKernelGGL(zd_k_jsum_blocks, dim3((a.n_jblk + 63) / 64), dim3(64), 0, s, (const FrameState*)fstate,
                        blocks, comp, (const CompState*)cstate, jframes, jd, a.n_jblk, jb, jseg);
-    hipLaunchKernelGGL(zd_k_jprefix, dim3(a.n_jframes), dim3(64), 0, s, frames, fstate, jframes, jd, jb);
+    hipLaunchKernelGGL(zd_k_jprefix, dim3(a.n_jframes), dim3(64 * JP_WAVES), 0, s, frames, fstate, jframes, jd, jb);
     hipLaunchKernelGGL(zd_k_jscatter, dim3(a.n_jseg), dim3(64), 0, s, a.src, fstate, blocks, comp,
                        (const CompState*)cstate, (const uint8_t*)(ws + W.lits), (const uint64_t*)seqs,
                        (const uint16_t*)fses, jframes, jd, (const JBlk*)jb, (const JSeg*)jseg, jsd, jst);
