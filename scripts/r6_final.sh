@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 end check at HEAD: the whole GPU suite, smoke, the default bench
-# line (C4) and the c3s line, each step under its own limit.
+# line (C4), the c3s, C3, C2 and C5 level-1 lines, each step under its own limit.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -15,4 +15,5 @@ timeout -k 10 600 python bench.py > gpurun_out/fin_c4.json 2> gpurun_out/fin_c4.
 timeout -k 10 600 python bench.py --workload c3s > gpurun_out/fin_c3s.json 2> gpurun_out/fin_c3s.err || exit 1
 timeout -k 10 600 python bench.py --workload c3 > gpurun_out/fin_c3.json 2> gpurun_out/fin_c3.err || exit 1
 timeout -k 10 600 python bench.py --workload c2 > gpurun_out/fin_c2.json 2> gpurun_out/fin_c2.err || exit 1
-for w in c4 c3s c3 c2; do python -c "import json; d=json.load(open('gpurun_out/fin_$w.json')); print('$w', d['value'], d['ms_per_step'], d['roofline']['kernel'][:30], d['roofline']['kernel_ms'], d['roofline']['frac'], d['verified_bit_exact'], d['cpu_baseline']['value'])"; done
+timeout -k 10 600 python bench.py --workload c5 --level 1 > gpurun_out/fin_c5.json 2> gpurun_out/fin_c5.err || exit 1
+for w in c4 c3s c3 c2 c5; do python -c "import json; d=json.load(open('gpurun_out/fin_$w.json')); print('$w', d['value'], d['ms_per_step'], d['roofline']['kernel'][:30], d['roofline']['kernel_ms'], d['roofline']['frac'], d['verified_bit_exact'], d['cpu_baseline']['value'])"; done
