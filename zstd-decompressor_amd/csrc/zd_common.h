@@ -433,7 +433,11 @@ constexpr uint32_t J_FINAL = 1u << 31;
 constexpr int J_MAX_ROUNDS = 40;
 // sequences per K4J scatter segment (one wave each; c3s: 1024 -> 512 took the
 // scatter from 0.33 to 0.29 ms, the segment sums 9 -> 15 us; 256 no better)
-constexpr uint32_t J_SEG = 512;
+#ifndef ZD_J_SEG
+#define ZD_J_SEG 512
+#endif
+constexpr uint32_t J_SEG = ZD_J_SEG;
+static_assert(J_SEG % 64 == 0, "a scatter segment is whole 64-sequence batches");
 struct JFrame {
   uint64_t base;           // word index of the frame's region in the state array
   uint64_t cap;            // words of the region (>= the frame's capacity)
